@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: Mray-samples/s of the MI355X render loop (BASELINE.json metric).
+
+One step = one full frame of the workload (default: box_scene.hpp at
+1920x1080, 1024 spp = 256 samples per sub-pixel) rendered by the HIP
+megakernel, scene and output already resident in HBM.  With N ranks
+(torchrun, one process per GPU) the frame is tile-sharded by interleaved row
+bands and the step includes the single gather (RCCL over xGMI) to rank 0 and
+the un-shard; value = whole-frame samples / max-over-ranks time (strong
+scaling: the frame size is fixed).
+
+Also reported:
+  roofline     -- VALU fp32 roofline of the render kernel: algorithmic FLOP
+                  per launch (S_bar*(23*N_spheres + 100) + 60 per sample,
+                  SURVEY.md 8(d), S_bar measured by the kernel's own segment
+                  counter) / its average launch time from HIP events on the
+                  launch stream; peak 157.3 TFLOP/s (MI355X fp32 vector).
+  cpu_baseline -- the repo's own OpenMP CPU loop (oracle/, the reference
+                  algorithm in double + mt19937, "port") on a bounded sample
+                  of the same workload, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cpu-path-tracing_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import ptgpu  # noqa: E402
+
+METRIC = "Mray-samples/sec at 1920×1080×1024spp; per-pixel RMSE vs CPU ref"
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s):
+    """Time the repo's OpenMP CPU path (oracle Mode A: reference arithmetic,
+    double + mt19937 row seeding) on a bounded subset of the frame's rows."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import pyoracle as po
+        po.lib()
+    except Exception as e:  # noqa: BLE001
+        log(f"cpu_baseline unavailable: {e}")
+        return None
+    scn = ptgpu.make_scene(scene_name, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    sp = scn.to_array().view(po.SPHERE_DT)
+    ca = cam.to_array().view(po.CAMERA_DT)
+    img = np.zeros(W * H * 3)
+    rows = 0
+    t0 = time.perf_counter()
+    offsets = []
+    for k in range(0, 64, 8):  # row sets y = k, k+64, k+128, ...
+        for kk in (k, k + 4):
+            n = len(range(kk, H, 64))
+            rc = po.lib().po_render_mt(po.ptr(sp), len(sp), po.ptr(ca), W, H, samps, nsub, 1, kk, H, 64, threads,
+                                       po.ptr(img))
+            assert rc == 0
+            rows += n
+            offsets.append(kk)
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    nsamp = rows * W * samps * nsub * nsub
+    return {"value": round(nsamp / dt / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "port",
+            "seconds": round(dt, 2),
+            "sample": (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp, {rows} of {H} rows "
+                       f"(y = k mod 64 for k in {offsets}); oracle Mode A (double, mt19937 per row, "
+                       f"reference arithmetic) in an OpenMP schedule(dynamic,1) row loop")}
+
+
+def load_traffic(workload):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="box")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024, help="total samples per pixel (4 sub-pixels)")
+    ap.add_argument("--band-rows", type=int, default=ptgpu.DEFAULT_BAND_ROWS)
+    ap.add_argument("--chunk", type=int, default=0, help="samples per sub-pixel per work unit (0 = auto)")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    nsub = 2  # main.cpp:202
+    W, H = args.width, args.height
+    samps = args.spp // (nsub * nsub)  # main.cpp:206
+    spp = samps * nsub * nsub
+    scn = ptgpu.make_scene(args.scene, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    ctx = ptgpu.Context(scn, cam, device=local)
+    params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk)
+    rows = ptgpu.shard_rows(H, args.band_rows, world)
+    slab = torch.zeros(rows * W * 3, dtype=torch.float32, device=dev)
+    my_rows = int((ptgpu.slab_to_image_rows(H, args.band_rows, rank, world) >= 0).sum())
+    segs = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(count=False, events=None):
+        if events is not None:
+            events[0].record(stream)
+        ctx.render_device(slab, params, segs if count else None, stream)
+        if events is not None:
+            events[1].record(stream)
+        if world > 1:
+            return ptgpu.render_sharded(params, slab, tile_renderer=lambda out, p: None)
+        return slab
+
+    # S_bar from the kernel's own segment counter (untimed)
+    step(count=True)
+    torch.cuda.synchronize()
+    seg_local = int(segs.item())
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events=evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if args.steps else float("nan")
+
+    seg_total = seg_local
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+        s = torch.tensor([seg_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(s)
+        seg_total = int(s.item())
+    frame_samples = W * H * spp
+    s_bar = seg_total / frame_samples
+    n_sph = ctx.n_spheres
+    flop_per_sample = s_bar * (23 * n_sph + 100) + 60
+    my_samples = my_rows * W * spp
+    achieved = my_samples * flop_per_sample / (kern_ms / 1e3) / 1e12 if kern_ms > 0 else None
+
+    if rank == 0:
+        workload = f"{args.scene} {W}x{H} {spp}spp"
+        value = frame_samples * args.steps / elapsed / 1e6
+        cpu = None
+        if world == 1 and args.cpu_baseline == "auto":
+            cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads, args.cpu_seconds)
+        traffic = load_traffic(workload)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mray-samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural scene from the reference's box_scene.hpp; counter-RNG seed 0x5EED0001)",
+            "config": {"workload": workload, "scene": args.scene, "width": W, "height": H, "spp": spp,
+                       "samples_per_subpixel": samps, "num_subpixels": nsub, "spheres": n_sph,
+                       "band_rows": args.band_rows, "chunk_samples": args.chunk or "auto",
+                       "parallelism": f"tile-sharded row bands x{world}" if world > 1 else "single GPU"},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3) if achieved else None,
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
+                         "traffic": traffic,
+                         "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
+                         "segments_per_sample": round(s_bar, 4)},
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+// pt_device.hpp -- device-side math of the MI355X render loop (gfx950).
+//
+// fp32 restatement of the reference's hot path, written so that every value
+// is produced by a fixed sequence of IEEE-754 operations (explicit fmaf,
+// correctly-rounded division and square root, a polynomial sin/cos), which
+// the oracle's Mode B (oracle/pt_oracle.c) executes on the host in the same
+// order -- the GPU image equals the CPU image bit-for-bit.  Compiled with
+// -ffp-contract=off: nothing fuses unless fmaf is written.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptg {
+
+// constants.hpp:7-10, main.cpp:106
+constexpr float kEps = 1e-4f;
+constexpr float kInf = 1e20f;
+constexpr int kDepthLimit = 100;
+constexpr int kRRThreshold = 4;
+
+struct f3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+__device__ __forceinline__ f3 sub3(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+// vec.cpp:35-38: x * (1 / sqrt(x.x)) -- IEEE sqrt then IEEE reciprocal-by-division
+__device__ __forceinline__ f3 norm3(f3 a)
+{
+    float inv = 1.0f / __builtin_sqrtf(dot3(a, a));
+    return mk3(a.x * inv, a.y * inv, a.z * inv);
+}
+__device__ __forceinline__ f3 cross3(f3 a, f3 b)
+{
+    return mk3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+               __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+}
+
+// ---- counter RNG: replaces pt::rand_state (random_state.cpp:3-17) ----------
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t key_hash(uint64_t seed, uint64_t pixel_sub)
+{
+    return mix64(seed ^ mix64(pixel_sub + 1ull));
+}
+__device__ __forceinline__ uint32_t sample_state(uint64_t key, uint32_t sample)
+{
+    uint32_t st = (uint32_t)(mix64(key + ((uint64_t)sample + 1ull) * 0x9E3779B97F4A7C15ull) >> 32);
+    return st ? st : 0x6D2B79F5u;
+}
+// one U[0,1) draw: xorshift32 (13,17,5), top 24 bits
+__device__ __forceinline__ float draw(uint32_t &st)
+{
+    st ^= st << 13;
+    st ^= st >> 17;
+    st ^= st << 5;
+    return (float)(st >> 8) * 0x1p-24f;
+}
+
+// sin/cos of 2*pi*u, u in [0,1) (replaces libm at main.cpp:55): exact quadrant
+// split of 4u, Taylor polynomials of sin(pi/2 f) / cos(pi/2 f), f in [0,1).
+__device__ __forceinline__ void sincos2pi(float u, float &c, float &s)
+{
+    float v = u * 4.0f;
+    float qf = __builtin_floorf(v);
+    float f = v - qf;
+    int q = (int)qf & 3;
+    float f2 = f * f;
+    float ps = __builtin_fmaf(f2, 0x1.e8f434p-25f, -0x1.e3075p-19f);
+    ps = __builtin_fmaf(f2, ps, 0x1.507834p-13f);
+    ps = __builtin_fmaf(f2, ps, -0x1.32d2ccp-8f);
+    ps = __builtin_fmaf(f2, ps, 0x1.466bc6p-4f);
+    ps = __builtin_fmaf(f2, ps, -0x1.4abbcep-1f);
+    ps = __builtin_fmaf(f2, ps, 0x1.921fb6p+0f);
+    float sn = f * ps;
+    float pc = __builtin_fmaf(f2, -0x1.b6e25p-28f, 0x1.f9d38ap-22f);
+    pc = __builtin_fmaf(f2, pc, -0x1.a6d1f2p-16f);
+    pc = __builtin_fmaf(f2, pc, 0x1.e1f506p-11f);
+    pc = __builtin_fmaf(f2, pc, -0x1.55d3c8p-6f);
+    pc = __builtin_fmaf(f2, pc, 0x1.03c1fp-2f);
+    pc = __builtin_fmaf(f2, pc, -0x1.3bd3ccp+0f);
+    float cs = __builtin_fmaf(f2, pc, 1.0f);
+    // rotate by q quarter turns
+    float c1 = (q & 1) ? -sn : cs;
+    float s1 = (q & 1) ? cs : sn;
+    c = (q & 2) ? -c1 : c1;
+    s = (q & 2) ? -s1 : s1;
+}
+
+// Scene records prepared on the host (ptg_render.hip: prepare_scene).
+// Geometry, 32 B per sphere, read with wave-uniform (scalar) loads:
+//   g0 = {P.x, P.y, P.z, k1}, g1 = {N.x, N.y, N.z, k2}
+//   huge sphere (R >= 1000): P = C + R*n0 on the surface facing the camera,
+//     N = n0, k1 = R, k2 = 2R  -> hb = e.d + R (n0.d), c = e.e + 2R (e.n0)
+//     (exact algebraic rewrite of |o + t d - C| = R, fp32-safe at R = 1e6)
+//   otherwise: P = C, N = 0, k1 = -1 (flag), k2 = -R^2 -> hb = e.d, c = e.e - R^2
+// Shading, 64 B per sphere, gathered by hit id:
+//   s0 = {C.xyz, prob}, s1 = {emission.xyz, material}, s2 = {color.xyz, 0}, s3 = {color/prob .xyz, 0}
+struct GeoRec {
+    float4 g0, g1;
+};
+struct ShadeRec {
+    float4 s0, s1, s2, s3;
+};
+
+}  // namespace ptg

@@ -1,0 +1,841 @@
+// ptg_render.hip -- the MI355X render-loop megakernel and its C ABI (include/ptgpu.h).
+//
+// Replaces the reference's per-pixel hot path (src/main.cpp:214-236 and
+// below).  Mapping onto CDNA4:
+//  * one lane per (pixel, sub-pixel): lanes 4p..4p+3 of a wave are the
+//    2x2 sub-pixels of pixel p (main.cpp:226-232), 16 pixels per wave64;
+//  * each lane runs its `samples` paths back to back in ONE flat loop whose
+//    iteration is one bounce segment: a lane whose path ends (miss, Russian
+//    roulette, depth cap) accumulates it and immediately starts its next
+//    sample (per-lane path regeneration), so the wave keeps ~all lanes busy
+//    despite the geometric path-length tail;
+//  * the scene scan reads sphere records with wave-uniform scalar loads
+//    (s_load into SGPRs -- the SMEM broadcast path, no VGPRs or LDS cycles
+//    spent on the 8-sphere scenes) or, with PTG_SPHERES_LDS, stages them in
+//    LDS once per workgroup;
+//  * per-wave segment counts via ballot popcount, one atomic per wave;
+//  * sub-pixel combine by in-register cross-lane reads, then coalesced
+//    192-B stores (three lanes of each pixel write R, G, B).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ptgpu.h"
+#include "pt_device.hpp"
+
+using namespace ptg;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define PTG_HIP(call)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(PTG_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));           \
+    } while (0)
+
+constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr double kBigRadius = 1000.0;
+
+struct KArgs {
+    const GeoRec *geo;
+    const ShadeRec *shade;
+    int n;
+    // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
+    float pos_x, pos_y, pos_z;
+    float base_x, base_y, base_z;
+    float X_x, X_y, X_z;
+    float Y_x, Y_y, Y_z;
+    float lens;
+    // image / sampling
+    int W, H, samps, nsub, lanes_per_pixel, pixels_per_wave, waves_per_row;
+    int slab_rows, band_rows, shard_rank, shard_count;
+    float fW, fH, inv_samps, sub_len, inv_sub2;
+    unsigned long long seed;
+    int chunk, n_groups, single_chunk;
+    long long n_units;
+    float *out;
+    unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
+    unsigned long long *segments;
+};
+
+struct Lane {
+    int x, y, sx, sy;
+    uint64_t key;
+};
+
+__device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32_t sample, uint32_t &st, f3 &o,
+                                           f3 &d)
+{
+    st = sample_state(L.key, sample);
+    // main.cpp:186-190: jitter inside the sub-pixel cell
+    float u1 = draw(st);
+    float u2 = draw(st);
+    float xin = __builtin_fmaf(A.sub_len, u1, (float)L.x + (float)L.sx * A.sub_len);
+    float yin = __builtin_fmaf(A.sub_len, u2, (float)L.y + (float)L.sy * A.sub_len);
+    float fs = xin / A.fW;
+    float ft = yin / A.fH;
+    // camera.cpp:19-30: rejection sample of the unit disk (2 draws per try)
+    float px, py;
+    do {
+        px = __builtin_fmaf(2.0f, draw(st), -1.0f);
+        py = __builtin_fmaf(2.0f, draw(st), -1.0f);
+    } while (__builtin_fmaf(py, py, px * px) >= 1.0f);
+    // camera.cpp:34-37 (offset = rd*s + rd*t, the reference's lens quirk)
+    float sst = fs + ft;
+    float ox = (px * A.lens) * sst;
+    float oy = (py * A.lens) * sst;
+    o = mk3(A.pos_x + ox, A.pos_y + oy, A.pos_z);
+    d = mk3(__builtin_fmaf(A.Y_x, ft, __builtin_fmaf(A.X_x, fs, A.base_x)) - ox,
+            __builtin_fmaf(A.Y_y, ft, __builtin_fmaf(A.X_y, fs, A.base_y)) - oy,
+            __builtin_fmaf(A.Y_z, ft, __builtin_fmaf(A.X_z, fs, A.base_z)));
+}
+
+// main.cpp:30-42 + sphere.cpp:6-30: closest root >= eps over all spheres,
+// strict < so the lowest index wins ties.  Sphere records are loaded with
+// wave-uniform addresses -> scalar loads.
+template <bool kLds>
+__device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
+{
+    float a = dot3(d, d);
+    float tb = kInf;
+    int id = -1;
+    for (int i = 0; i < A.n; ++i) {
+        float4 g0 = geo[i].g0;
+        float4 g1 = geo[i].g1;
+        f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
+        float ed = dot3(e, d);
+        float ee = dot3(e, e);
+        float hb, c;
+        if (g0.w >= 0.0f) {  // huge sphere: anchored form
+            hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
+            c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
+        } else {
+            hb = ed;
+            c = ee + g1.w;
+        }
+        float disc = __builtin_fmaf(hb, hb, -(a * c));
+        if (disc < 0.0f)
+            continue;
+        float sq = __builtin_sqrtf(disc);
+        float q = -(hb + __builtin_copysignf(sq, hb));
+        float t1 = q / a;
+        float t2 = c / q;
+        float tmin = t1 < t2 ? t1 : t2;
+        float tmax = t1 < t2 ? t2 : t1;
+        float root = tmin;
+        if (root < kEps) {
+            root = tmax;
+            if (root < kEps)
+                continue;
+        }
+        if (root > 0.0f && root < tb) {
+            tb = root;
+            id = i;
+        }
+    }
+    tbest = tb;
+    return id;
+}
+
+// Per-lane state machine: one call = one bounce segment of radiance()
+// (main.cpp:111-155).  Returns true when the path has ended; E then holds
+// its radiance.
+template <bool kLds>
+__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o, f3 &d, f3 &T, f3 &E, int &depth,
+                                        uint32_t &st)
+{
+    float t;
+    int id = scene_scan<kLds>(A, geo, o, d, t);
+    if (id < 0) {  // main.cpp:115-120: sky
+        f3 ud = norm3(d);
+        float tt = 0.5f * (ud.y + 1.0f);
+        float it = 1.0f - tt;
+        E = mk3(__builtin_fmaf(T.x, __builtin_fmaf(tt, 0.5f, it), E.x),
+                __builtin_fmaf(T.y, __builtin_fmaf(tt, 0.7f, it), E.y),
+                __builtin_fmaf(T.z, __builtin_fmaf(tt, 1.0f, it), E.z));
+        return true;
+    }
+    const ShadeRec &S = A.shade[id];
+    float4 s0 = S.s0, s1 = S.s1;
+    // hit_record.cpp:3-12
+    f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
+    f3 on = norm3(mk3(p.x - s0.x, p.y - s0.y, p.z - s0.z));
+    bool front = dot3(on, d) < 0.0f;
+    f3 nn = front ? on : mk3(-on.x, -on.y, -on.z);
+    // main.cpp:126
+    E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
+    // main.cpp:128-139: Russian roulette after depth 4
+    float4 col;
+    if (depth > kRRThreshold) {
+        if (draw(st) < s0.w)
+            col = S.s3;
+        else
+            return true;
+    } else {
+        col = S.s2;
+    }
+    T = mk3(T.x * col.x, T.y * col.y, T.z * col.z);
+    int mat = __float_as_int(s1.w);
+    bool spec = mat == PTG_SPECULAR;
+    if (mat == PTG_DIFFUSE) {  // main.cpp:44-58
+        float u_phi = draw(st);
+        float ra = draw(st);
+        float cp, sp;
+        sincos2pi(u_phi, cp, sp);
+        float sth = __builtin_sqrtf(ra);
+        float cth = __builtin_sqrtf(1.0f - ra);
+        f3 w = nn;
+        f3 uu = __builtin_fabsf(w.x) > 0.1f ? mk3(w.z, 0.0f, -w.x) : mk3(0.0f, -w.z, w.y);
+        uu = norm3(uu);
+        f3 vv = cross3(w, uu);
+        float cs = cp * sth, ss = sp * sth;
+        f3 nd = mk3(__builtin_fmaf(w.x, cth, __builtin_fmaf(vv.x, ss, uu.x * cs)),
+                    __builtin_fmaf(w.y, cth, __builtin_fmaf(vv.y, ss, uu.y * cs)),
+                    __builtin_fmaf(w.z, cth, __builtin_fmaf(vv.z, ss, uu.z * cs)));
+        o = p;
+        d = norm3(nd);
+    } else if (mat == PTG_DIELECTRIC) {  // main.cpp:69-97
+        float ratio = front ? 0.5f : 2.0f;
+        f3 ud = norm3(d);
+        float x0 = -dot3(ud, nn);
+        float cth = 1.0f < x0 ? 1.0f : x0;
+        float sth = __builtin_sqrtf(__builtin_fmaf(-cth, cth, 1.0f));
+        bool reflect = ratio * sth > 1.0f;  // cannot refract: no Fresnel draw
+        if (!reflect) {
+            float r0 = (1.0f - ratio) / (1.0f + ratio);
+            r0 = r0 * r0;
+            float xm = 1.0f - cth;
+            float x2 = xm * xm;
+            float x5 = (x2 * x2) * xm;
+            float R = __builtin_fmaf(1.0f - r0, x5, r0);
+            reflect = R > draw(st);
+        }
+        if (reflect) {
+            spec = true;
+        } else {
+            f3 perp = mk3(__builtin_fmaf(nn.x, cth, ud.x) * ratio, __builtin_fmaf(nn.y, cth, ud.y) * ratio,
+                          __builtin_fmaf(nn.z, cth, ud.z) * ratio);
+            float sq = __builtin_sqrtf(__builtin_fabsf(1.0f - dot3(perp, perp)));
+            o = p;
+            d = mk3(__builtin_fmaf(nn.x, -sq, perp.x), __builtin_fmaf(nn.y, -sq, perp.y),
+                    __builtin_fmaf(nn.z, -sq, perp.z));
+        }
+    }
+    if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
+        float k = dot3(on, d);
+        k = k + k;
+        (void)draw(st);
+        o = p;
+        d = mk3(__builtin_fmaf(-k, on.x, d.x), __builtin_fmaf(-k, on.y, d.y), __builtin_fmaf(-k, on.z, d.z));
+    }
+    depth += 1;
+    return depth >= kDepthLimit;
+}
+
+// Slab row -> image (output) row for the band shard.
+__device__ __forceinline__ int out_row_of(const KArgs &A, int slab_row)
+{
+    int band = slab_row / A.band_rows;
+    return (band * A.shard_count + A.shard_rank) * A.band_rows + (slab_row - band * A.band_rows);
+}
+
+// Exact per-path quantisation (include/ptgpu.h "Sample accumulation").
+__device__ __forceinline__ unsigned long long quant(float c)
+{
+    if (!(c >= 0.0f))
+        return 0ull;
+    if (c > 0x1p30f)
+        c = 0x1p30f;
+    return (unsigned long long)((double)c * 0x1p32);
+}
+
+// One work unit per wave: a pixel group (pixels_per_wave pixels of one slab
+// row, all their sub-pixels = up to 64 "slots") x one chunk of samples.
+// The unit's nv*cnt paths form a pool: every lane starts one path, and a lane
+// whose path ends takes the next unstarted path of the pool (ballot + rank),
+// so all lanes stay busy until the pool is empty.  Path radiance is
+// accumulated exactly (u64) per slot in LDS and added to the global
+// accumulator once per unit.
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void render_kernel(KArgs A)
+{
+    __shared__ unsigned long long lds_acc[kWavesPerBlock][64 * 3];
+    __shared__ unsigned long long lds_key[kWavesPerBlock][64];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const long long unit = (long long)blockIdx.x * kWavesPerBlock + wv;
+    if (unit >= A.n_units)
+        return;  // whole wave
+    const int group = (int)(unit % A.n_groups);  // chunk-major: neighbours are different pixel groups
+    const int chunk = (int)(unit / A.n_groups);
+    const int slab_row = group / A.waves_per_row;
+    const int xblk = group - slab_row * A.waves_per_row;
+    const int r = out_row_of(A, slab_row);
+    const int y = A.H - 1 - r;  // main.cpp:181: y = 0 is the bottom row
+    const int x0 = xblk * A.pixels_per_wave;
+    int npix = A.W - x0;
+    npix = npix < A.pixels_per_wave ? npix : A.pixels_per_wave;
+    const int nv = r < A.H ? npix * A.lanes_per_pixel : 0;  // valid slots are a prefix
+    const int s0 = chunk * A.chunk;
+    int cnt = A.samps - s0;
+    cnt = cnt < A.chunk ? cnt : A.chunk;
+    const int total = nv * cnt;
+
+    lds_acc[wv][lane] = 0ull;
+    lds_acc[wv][lane + 64] = 0ull;
+    lds_acc[wv][lane + 128] = 0ull;
+    if (lane < nv) {
+        int px = x0 + lane / A.lanes_per_pixel;
+        int sub = lane % A.lanes_per_pixel;
+        uint64_t ps = ((uint64_t)y * (uint64_t)A.W + (uint64_t)px) * (uint64_t)A.lanes_per_pixel + (uint64_t)sub;
+        lds_key[wv][lane] = key_hash(A.seed, ps);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    int item = lane < total ? lane : -1;
+    int slot = 0;
+    f3 o, d, T, E;
+    int depth = 0;
+    uint32_t st = 0;
+    uint32_t segs = 0;
+    auto start = [&](int it) {
+        slot = it % nv;
+        int sample = s0 + it / nv;
+        Lane L;
+        int ps = slot / A.lanes_per_pixel;
+        int sub = slot - ps * A.lanes_per_pixel;
+        L.x = x0 + ps;
+        L.y = y;
+        L.sy = sub / A.nsub;
+        L.sx = sub - L.sy * A.nsub;
+        L.key = lds_key[wv][slot];
+        camera_ray(A, L, (uint32_t)sample, st, o, d);
+        T = mk3(1.0f, 1.0f, 1.0f);
+        E = mk3(0.0f, 0.0f, 0.0f);
+        depth = 0;
+    };
+    if (item >= 0)
+        start(item);
+    int next = total < 64 ? total : 64;  // wave-uniform pool cursor
+    // flat loop: one iteration = one bounce segment for every live lane
+    while (__ballot(item >= 0) != 0ull) {
+        bool done = false;
+        if (item >= 0) {
+            if constexpr (kCount)
+                segs += 1;
+            done = segment<false>(A, A.geo, o, d, T, E, depth, st);
+            if (done) {
+                atomicAdd(&lds_acc[wv][slot], quant(E.x));
+                atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
+                atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
+            }
+        }
+        const unsigned long long dm = __ballot(done);
+        if (done) {
+            int ni = next + (int)__popcll(dm & ((1ull << lane) - 1ull));
+            item = ni < total ? ni : -1;
+            if (item >= 0)
+                start(item);
+        }
+        next += (int)__popcll(dm);
+    }
+    if constexpr (kCount) {
+        unsigned long long ws = segs;
+        for (int off = 32; off > 0; off >>= 1)
+            ws += __shfl_xor(ws, off, 64);
+        if (lane == 0 && ws)
+            atomicAdd(A.segments, ws);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nv) {
+        unsigned long long *g = A.acc + (((size_t)slab_row * A.W + x0) * A.lanes_per_pixel + lane) * 3;
+        unsigned long long vx = lds_acc[wv][lane], vy = lds_acc[wv][lane + 64], vz = lds_acc[wv][lane + 128];
+        if (A.single_chunk) {  // sole writer of these sums: plain stores
+            g[0] = vx;
+            g[1] = vy;
+            g[2] = vz;
+        } else {
+            if (vx) atomicAdd(g + 0, vx);
+            if (vy) atomicAdd(g + 1, vy);
+            if (vz) atomicAdd(g + 2, vz);
+        }
+    }
+}
+
+// main.cpp:195-196: per pixel, the clamped sub-pixel means added with weight
+// 1/nsub^2 in (sy, sx) order; re-zeroes the accumulator for the next frame.
+__global__ __launch_bounds__(256) void resolve_kernel(KArgs A)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)A.slab_rows * A.W)
+        return;
+    const int slab_row = (int)(i / A.W);
+    if (out_row_of(A, slab_row) >= A.H)
+        return;
+    unsigned long long *g = A.acc + (size_t)i * A.lanes_per_pixel * 3;
+    f3 pix = mk3(0.0f, 0.0f, 0.0f);
+    for (int j = 0; j < A.lanes_per_pixel; ++j) {
+        float m[3];
+        for (int c = 0; c < 3; ++c) {
+            unsigned long long sum = g[3 * j + c];
+            g[3 * j + c] = 0ull;
+            float mean = A.samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)A.samps) : 0.0f;
+            m[c] = mean < 0.0f ? 0.0f : (1.0f < mean ? 1.0f : mean);
+        }
+        pix = mk3(__builtin_fmaf(m[0], A.inv_sub2, pix.x), __builtin_fmaf(m[1], A.inv_sub2, pix.y),
+                  __builtin_fmaf(m[2], A.inv_sub2, pix.z));
+    }
+    float *out = A.out + (size_t)i * 3;
+    out[0] = pix.x;
+    out[1] = pix.y;
+    out[2] = pix.z;
+}
+
+// Parity probe: one path per record {x, y, sx, sy, sample}.
+__global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *coords, int n, float *out,
+                                                         int32_t *segs_out)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    Lane L;
+    L.x = coords[5 * i + 0];
+    L.y = coords[5 * i + 1];
+    L.sx = coords[5 * i + 2];
+    L.sy = coords[5 * i + 3];
+    uint32_t sample = (uint32_t)coords[5 * i + 4];
+    uint64_t pixel_sub = ((uint64_t)L.y * (uint64_t)A.W + (uint64_t)L.x) * (uint64_t)A.lanes_per_pixel +
+                         (uint64_t)(L.sy * A.nsub + L.sx);
+    L.key = key_hash(A.seed, pixel_sub);
+    f3 o, d;
+    uint32_t st;
+    camera_ray(A, L, sample, st, o, d);
+    f3 T = mk3(1.0f, 1.0f, 1.0f), E = mk3(0.0f, 0.0f, 0.0f);
+    int depth = 0, segs = 0;
+    bool done = false;
+    while (!done) {
+        segs += 1;
+        done = segment<false>(A, A.geo, o, d, T, E, depth, st);
+    }
+    out[3 * i + 0] = E.x;
+    out[3 * i + 1] = E.y;
+    out[3 * i + 2] = E.z;
+    segs_out[i] = segs;
+}
+
+__global__ void unshard_kernel(const float *__restrict__ src, float *__restrict__ dst, int W, int band_rows,
+                               int count, int slab_rows)
+{
+    int r = blockIdx.y;
+    int band = r / band_rows;
+    int k = band % count;
+    int j = band / count;
+    size_t srow = (size_t)k * slab_rows + (size_t)j * band_rows + (size_t)(r - band * band_rows);
+    const float *s = src + srow * (size_t)W * 3;
+    float *t = dst + (size_t)r * (size_t)W * 3;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < W * 3; i += gridDim.x * blockDim.x)
+        t[i] = s[i];
+}
+
+// utils.cpp:11-16: round(pow(clamp(x), 1/2.2) * 255)
+__global__ void tonemap_kernel(const float *__restrict__ in, uint8_t *__restrict__ out, size_t count)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count)
+        return;
+    double x = (double)in[i];
+    x = x < 0.0 ? 0.0 : (1.0 < x ? 1.0 : x);
+    out[i] = (uint8_t)(int)round(pow(x, 1.0 / 2.2) * 255.0);
+}
+
+}  // namespace
+
+struct ptg_context {
+    int device;
+    int n;
+    GeoRec *d_geo;
+    ShadeRec *d_shade;
+    unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
+    size_t acc_elems;
+    KArgs base;  // camera + scene fields filled
+};
+
+namespace {
+
+bool sphere_ok(const ptg_sphere &s)
+{
+    if (!(s.radius > 0.0) || !std::isfinite(s.radius))
+        return false;
+    for (int c = 0; c < 3; ++c)
+        if (!std::isfinite(s.position[c]) || !std::isfinite(s.emission[c]) || !std::isfinite(s.color[c]))
+            return false;
+    return s.material >= PTG_DIFFUSE && s.material <= PTG_DIELECTRIC;
+}
+
+// Host-side preparation (double -> fp32 records), the counterpart of the
+// oracle's Mode B prep_B; the anchor for huge spheres is the camera position.
+void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vector<GeoRec> &geo,
+                   std::vector<ShadeRec> &shade)
+{
+    geo.resize(n);
+    shade.resize(n);
+    for (int i = 0; i < n; ++i) {
+        const ptg_sphere &sp = s[i];
+        const double R = sp.radius;
+        GeoRec g;
+        if (R >= kBigRadius) {
+            double vx = cam->position[0] - sp.position[0];
+            double vy = cam->position[1] - sp.position[1];
+            double vz = cam->position[2] - sp.position[2];
+            double len = std::sqrt(vx * vx + vy * vy + vz * vz);
+            double nx = 0.0, ny = 1.0, nz = 0.0;
+            if (len > 0.0) {
+                nx = vx / len;
+                ny = vy / len;
+                nz = vz / len;
+            }
+            g.g0 = make_float4((float)(sp.position[0] + R * nx), (float)(sp.position[1] + R * ny),
+                               (float)(sp.position[2] + R * nz), (float)R);
+            g.g1 = make_float4((float)nx, (float)ny, (float)nz, (float)(2.0 * R));
+        } else {
+            g.g0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], -1.0f);
+            g.g1 = make_float4(0.0f, 0.0f, 0.0f, (float)(-(R * R)));
+        }
+        geo[i] = g;
+        ShadeRec r;
+        float cx = (float)sp.color[0], cy = (float)sp.color[1], cz = (float)sp.color[2];
+        float p = cx;
+        if (p < cy) p = cy;
+        if (p < cz) p = cz;
+        float rx = 0.0f, ry = 0.0f, rz = 0.0f;
+        if (p > 0.0f) {
+            float inv = 1.0f / p;
+            rx = cx * inv;
+            ry = cy * inv;
+            rz = cz * inv;
+        }
+        int32_t mat = sp.material;
+        float matf;
+        std::memcpy(&matf, &mat, 4);
+        r.s0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], p);
+        r.s1 = make_float4((float)sp.emission[0], (float)sp.emission[1], (float)sp.emission[2], matf);
+        r.s2 = make_float4(cx, cy, cz, 0.0f);
+        r.s3 = make_float4(rx, ry, rz, 0.0f);
+        shade[i] = r;
+    }
+}
+
+int check_params(const ptg_params *p)
+{
+    if (!p)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "params is NULL");
+    if (p->width <= 0 || p->height <= 0)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "width and height must be positive");
+    if (p->samples < 0)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "samples must be >= 0");
+    if (p->num_subpixels < 1 || p->num_subpixels > 8)
+        return fail(PTG_ERR_UNSUPPORTED, "num_subpixels must be in [1, 8]");
+    if (p->band_rows < 1 || p->shard_count < 1 || p->shard_rank < 0 || p->shard_rank >= p->shard_count)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "invalid shard (band_rows >= 1, 0 <= rank < count)");
+    if ((int64_t)p->width * p->height > (int64_t)1 << 28)
+        return fail(PTG_ERR_UNSUPPORTED, "image too large");
+    return PTG_OK;
+}
+
+void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid)
+{
+    A = ctx->base;
+    A.W = p->width;
+    A.H = p->height;
+    A.samps = p->samples;
+    A.nsub = p->num_subpixels;
+    A.lanes_per_pixel = p->num_subpixels * p->num_subpixels;
+    A.pixels_per_wave = 64 / A.lanes_per_pixel;
+    A.waves_per_row = (p->width + A.pixels_per_wave - 1) / A.pixels_per_wave;
+    int bands = (p->height + p->band_rows - 1) / p->band_rows;
+    A.slab_rows = ((bands + p->shard_count - 1) / p->shard_count) * p->band_rows;
+    A.band_rows = p->band_rows;
+    A.shard_rank = p->shard_rank;
+    A.shard_count = p->shard_count;
+    A.fW = (float)p->width;
+    A.fH = (float)p->height;
+    A.inv_samps = p->samples > 0 ? 1.0f / (float)p->samples : 0.0f;
+    A.sub_len = 1.0f / (float)p->num_subpixels;
+    A.inv_sub2 = 1.0f / (float)(p->num_subpixels * p->num_subpixels);
+    A.seed = p->seed;
+    // work unit = pixel group x chunk of samples (auto: 32 samples per sub-pixel)
+    int chunk = p->chunk_samples > 0 ? p->chunk_samples : 32;
+    if (chunk > p->samples)
+        chunk = p->samples > 0 ? p->samples : 1;
+    A.chunk = chunk;
+    A.n_groups = A.slab_rows * A.waves_per_row;
+    int n_chunks = p->samples > 0 ? (p->samples + chunk - 1) / chunk : 0;
+    A.single_chunk = n_chunks <= 1;
+    A.n_units = (long long)A.n_groups * n_chunks;
+    grid = (int)((A.n_units + kWavesPerBlock - 1) / kWavesPerBlock);
+}
+
+int set_device(int device)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(PTG_ERR_NO_DEVICE, "no HIP device visible");
+    if (device >= count)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "device ordinal out of range");
+    if (device >= 0)
+        PTG_HIP(hipSetDevice(device));
+    return PTG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptg_abi_version(void) { return PTG_ABI_VERSION; }
+
+const char *ptg_last_error(void) { return g_last_error.c_str(); }
+
+int ptg_device_count(int *count)
+{
+    if (!count)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "count is NULL");
+    *count = 0;
+    if (hipGetDeviceCount(count) != hipSuccess)
+        *count = 0;
+    return PTG_OK;
+}
+
+int ptg_shard_rows(int32_t height, int32_t band_rows, int32_t shard_count, int32_t *rows)
+{
+    if (!rows || height <= 0 || band_rows <= 0 || shard_count <= 0)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "invalid shard geometry");
+    int bands = (height + band_rows - 1) / band_rows;
+    *rows = ((bands + shard_count - 1) / shard_count) * band_rows;
+    return PTG_OK;
+}
+
+int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int device,
+                       ptg_context **out)
+{
+    if (!out || !cam || (n_spheres && !spheres))
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out = nullptr;
+    if (n_spheres > (size_t)(1 << 24))
+        return fail(PTG_ERR_UNSUPPORTED, "too many spheres");
+    for (size_t i = 0; i < n_spheres; ++i)
+        if (!sphere_ok(spheres[i]))
+            return fail(PTG_ERR_INVALID_ARGUMENT, "sphere " + std::to_string(i) + " is invalid");
+    int rc = set_device(device);
+    if (rc)
+        return rc;
+    int dev = 0;
+    PTG_HIP(hipGetDevice(&dev));
+    std::vector<GeoRec> geo;
+    std::vector<ShadeRec> shade;
+    prepare_scene(spheres, (int)n_spheres, cam, geo, shade);
+    ptg_context *ctx = new ptg_context();
+    ctx->device = dev;
+    ctx->n = (int)n_spheres;
+    size_t ng = std::max<size_t>(n_spheres, 1);
+    if (hipMalloc(&ctx->d_geo, ng * sizeof(GeoRec)) != hipSuccess ||
+        hipMalloc(&ctx->d_shade, ng * sizeof(ShadeRec)) != hipSuccess) {
+        (void)hipFree(ctx->d_geo);
+        delete ctx;
+        return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the scene failed");
+    }
+    if (n_spheres) {
+        PTG_HIP(hipMemcpy(ctx->d_geo, geo.data(), n_spheres * sizeof(GeoRec), hipMemcpyHostToDevice));
+        PTG_HIP(hipMemcpy(ctx->d_shade, shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
+    }
+    KArgs &A = ctx->base;
+    std::memset(&A, 0, sizeof(A));
+    A.geo = ctx->d_geo;
+    A.shade = ctx->d_shade;
+    A.n = (int)n_spheres;
+    A.pos_x = (float)cam->position[0];
+    A.pos_y = (float)cam->position[1];
+    A.pos_z = (float)cam->position[2];
+    A.base_x = (float)(cam->lower_left_corner[0] - cam->position[0]);
+    A.base_y = (float)(cam->lower_left_corner[1] - cam->position[1]);
+    A.base_z = (float)(cam->lower_left_corner[2] - cam->position[2]);
+    A.X_x = (float)cam->cam_x_axis[0];
+    A.X_y = (float)cam->cam_x_axis[1];
+    A.X_z = (float)cam->cam_x_axis[2];
+    A.Y_x = (float)cam->cam_y_axis[0];
+    A.Y_y = (float)cam->cam_y_axis[1];
+    A.Y_z = (float)cam->cam_y_axis[2];
+    A.lens = (float)cam->lens_radius;
+    *out = ctx;
+    return PTG_OK;
+}
+
+int ptg_context_destroy(ptg_context *ctx)
+{
+    if (!ctx)
+        return PTG_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipFree(ctx->d_geo);
+    (void)hipFree(ctx->d_shade);
+    if (ctx->d_acc)
+        (void)hipFree(ctx->d_acc);
+    delete ctx;
+    return PTG_OK;
+}
+
+int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab, unsigned long long *d_segments,
+                      void *stream)
+{
+    if (!ctx || !d_slab)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL context or output");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    PTG_HIP(hipSetDevice(ctx->device));
+    KArgs A;
+    int grid = 0;
+    fill_launch(ctx, params, A, grid);
+    // exact accumulator: allocated (zeroed) on first use at a size, kept zero by resolve_kernel
+    size_t need = (size_t)A.slab_rows * A.W * A.lanes_per_pixel * 3;
+    if (need > ctx->acc_elems) {
+        if (ctx->d_acc)
+            PTG_HIP(hipFree(ctx->d_acc));
+        ctx->d_acc = nullptr;
+        ctx->acc_elems = 0;
+        if (hipMalloc(&ctx->d_acc, need * sizeof(unsigned long long)) != hipSuccess)
+            return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the accumulator failed");
+        PTG_HIP(hipMemset(ctx->d_acc, 0, need * sizeof(unsigned long long)));
+        ctx->acc_elems = need;
+    }
+    A.out = d_slab;
+    A.acc = ctx->d_acc;
+    A.segments = d_segments;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (grid > 0) {
+        if (d_segments)
+            render_kernel<true><<<grid, kBlock, 0, s>>>(A);
+        else
+            render_kernel<false><<<grid, kBlock, 0, s>>>(A);
+        PTG_HIP(hipGetLastError());
+    }
+    long long pixels = (long long)A.slab_rows * A.W;
+    resolve_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>(A);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const int32_t *d_coords, size_t n,
+                             float *d_out, int32_t *d_segs, void *stream)
+{
+    if (!ctx || (n && (!d_coords || !d_out || !d_segs)))
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL argument");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    if (n == 0)
+        return PTG_OK;
+    PTG_HIP(hipSetDevice(ctx->device));
+    KArgs A;
+    int grid = 0;
+    fill_launch(ctx, params, A, grid);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int blocks = (int)((n + kBlock - 1) / kBlock);
+    trace_kernel<<<blocks, kBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int ptg_unshard_device(const float *d_gathered, float *d_image, int32_t width, int32_t height, int32_t band_rows,
+                       int32_t shard_count, void *stream)
+{
+    if (!d_gathered || !d_image || width <= 0 || height <= 0 || band_rows <= 0 || shard_count <= 0)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "invalid unshard arguments");
+    if (height > 65535)
+        return fail(PTG_ERR_UNSUPPORTED, "height > 65535");
+    int32_t slab_rows = 0;
+    ptg_shard_rows(height, band_rows, shard_count, &slab_rows);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int bx = std::max(1, std::min(64, (width * 3 + 255) / 256));
+    unshard_kernel<<<dim3(bx, height), 256, 0, s>>>(d_gathered, d_image, width, band_rows, shard_count, slab_rows);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int ptg_tonemap_device(const float *d_image, uint8_t *d_out, size_t count, void *stream)
+{
+    if (!d_image || !d_out)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (count == 0)
+        return PTG_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    size_t blocks = (count + 255) / 256;
+    tonemap_kernel<<<(unsigned)blocks, 256, 0, s>>>(d_image, d_out, count);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int ptg_render(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, const ptg_params *params,
+               int device, double *image_rgb)
+{
+    if (!image_rgb)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "image is NULL");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    ptg_context *ctx = nullptr;
+    rc = ptg_context_create(spheres, n_spheres, cam, device, &ctx);
+    if (rc)
+        return rc;
+    int32_t slab_rows = 0;
+    ptg_shard_rows(params->height, params->band_rows, params->shard_count, &slab_rows);
+    size_t slab_elems = (size_t)slab_rows * params->width * 3;
+    float *d_slab = nullptr;
+    std::vector<float> host(slab_elems);
+    rc = PTG_OK;
+    if (hipMalloc(&d_slab, slab_elems * sizeof(float)) != hipSuccess) {
+        ptg_context_destroy(ctx);
+        return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the image slab failed");
+    }
+    rc = ptg_render_device(ctx, params, d_slab, nullptr, nullptr);
+    if (rc == PTG_OK) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess)
+            e = hipMemcpy(host.data(), d_slab, slab_elems * sizeof(float), hipMemcpyDeviceToHost);
+        if (e != hipSuccess)
+            rc = fail(PTG_ERR_HIP, std::string("render: ") + hipGetErrorString(e));
+    }
+    (void)hipFree(d_slab);
+    ptg_context_destroy(ctx);
+    if (rc)
+        return rc;
+    const int W = params->width, H = params->height, BR = params->band_rows;
+    for (int j = 0; j < slab_rows; ++j) {
+        int band = j / BR;
+        int r = (band * params->shard_count + params->shard_rank) * BR + (j - band * BR);
+        if (r >= H)
+            continue;
+        const float *src = host.data() + (size_t)j * W * 3;
+        double *dst = image_rgb + (size_t)r * W * 3;
+        for (int i = 0; i < W * 3; ++i)
+            dst[i] = dst[i] + (double)src[i];  // main.cpp:196: image[row] += ...
+    }
+    return PTG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+"""ctypes binding of libptgpu.so (include/ptgpu.h).
+
+The product path: there is no fallback.  If the HIP library is missing or a
+call fails, a PtgError is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libptgpu.so")
+ABI_VERSION = 1
+
+# every symbol include/ptgpu.h declares
+EXPORTS = (
+    "ptg_abi_version", "ptg_last_error", "ptg_device_count", "ptg_render",
+    "ptg_context_create", "ptg_context_destroy", "ptg_shard_rows", "ptg_render_device",
+    "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
+)
+
+
+class PtgError(RuntimeError):
+    pass
+
+
+class Params(C.Structure):  # ptg_params
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("samples", C.c_int32),
+                ("num_subpixels", C.c_int32), ("seed", C.c_uint64), ("band_rows", C.c_int32),
+                ("shard_rank", C.c_int32), ("shard_count", C.c_int32), ("chunk_samples", C.c_int32),
+                ("flags", C.c_int32)]
+
+
+assert C.sizeof(Params) == 48
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PtgError(f"{LIB_PATH} not built: run `make -C cpu-path-tracing_amd` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        I = C.c_int
+        sig = {
+            "ptg_abi_version": (I, []),
+            "ptg_last_error": (C.c_char_p, []),
+            "ptg_device_count": (I, [C.POINTER(C.c_int)]),
+            "ptg_render": (I, [P, C.c_size_t, P, C.POINTER(Params), I, P]),
+            "ptg_context_create": (I, [P, C.c_size_t, P, I, C.POINTER(C.c_void_p)]),
+            "ptg_context_destroy": (I, [P]),
+            "ptg_shard_rows": (I, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
+            "ptg_render_device": (I, [P, C.POINTER(Params), P, P, P]),
+            "ptg_unshard_device": (I, [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
+            "ptg_tonemap_device": (I, [P, P, C.c_size_t, P]),
+            "ptg_trace_samples_device": (I, [P, C.POINTER(Params), P, C.c_size_t, P, P, P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.ptg_abi_version() != ABI_VERSION:
+            raise PtgError("libptgpu.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ptg_last_error().decode(errors="replace")
+        raise PtgError(f"{what} failed ({rc}): {msg}")

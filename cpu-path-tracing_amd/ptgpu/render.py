@@ -1,0 +1,208 @@
+"""Host-side render API over the C ABI.
+
+* render(...)            -- the drop-in for the reference's row loop
+                            (main.cpp:214-236): fills the caller's image
+                            (H*W RGB doubles, reference row order) exactly as
+                            the loop would, through ptg_render.
+* Context                -- device-resident scene for repeated renders into
+                            torch CUDA tensors (bench, multi-GPU).
+* render_sharded(...)    -- one process per GPU: each rank renders its
+                            interleaved row bands into a slab, one gather
+                            (RCCL over xGMI via torch.distributed) collects
+                            the slabs on rank 0, ptg_unshard_device restores
+                            the row order.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Optional
+
+import numpy as np
+
+from ._abi import Params, check, lib
+from .scene import CAMERA_DT, SPHERE_DT, camera, scene
+
+DEFAULT_SEED = 0x5EED0001
+DEFAULT_BAND_ROWS = 8
+
+
+def _spheres_array(scn) -> np.ndarray:
+    if isinstance(scn, scene):
+        return scn.to_array()
+    a = np.ascontiguousarray(scn)
+    if a.dtype != SPHERE_DT:
+        raise TypeError("spheres must be a ptgpu.scene or a SPHERE_DT array")
+    return a
+
+
+def _camera_array(cam) -> np.ndarray:
+    if isinstance(cam, camera):
+        return cam.to_array()
+    a = np.ascontiguousarray(cam).reshape(1)
+    if a.dtype != CAMERA_DT:
+        raise TypeError("cam must be a ptgpu.camera or a CAMERA_DT array")
+    return a
+
+
+def make_params(width, height, samples, num_subpixels=2, seed=DEFAULT_SEED, band_rows=DEFAULT_BAND_ROWS,
+                shard_rank=0, shard_count=1, chunk_samples=0) -> Params:
+    return Params(int(width), int(height), int(samples), int(num_subpixels), int(seed) & (2**64 - 1),
+                  int(band_rows), int(shard_rank), int(shard_count), int(chunk_samples), 0)
+
+
+def shard_rows(height: int, band_rows: int, shard_count: int) -> int:
+    out = C.c_int32(0)
+    check(lib().ptg_shard_rows(height, band_rows, shard_count, C.byref(out)), "ptg_shard_rows")
+    return out.value
+
+
+def slab_to_image_rows(height: int, band_rows: int, shard_rank: int, shard_count: int) -> np.ndarray:
+    """Output row of every slab row (-1 for padding), the mapping ptg_render_device uses."""
+    rows = shard_rows(height, band_rows, shard_count)
+    j = np.arange(rows)
+    band = j // band_rows
+    r = (band * shard_count + shard_rank) * band_rows + (j - band * band_rows)
+    return np.where(r < height, r, -1)
+
+
+def unshard_host(gathered: np.ndarray, width: int, height: int, band_rows: int, shard_count: int) -> np.ndarray:
+    """Host statement of ptg_unshard_device (rank-major slabs -> image rows)."""
+    rows = shard_rows(height, band_rows, shard_count)
+    g = np.asarray(gathered).reshape(shard_count * rows, width * 3)
+    out = np.zeros((height, width * 3), dtype=g.dtype)
+    for k in range(shard_count):
+        m = slab_to_image_rows(height, band_rows, k, shard_count)
+        ok = m >= 0
+        out[m[ok]] = g[k * rows:(k + 1) * rows][ok]
+    return out.reshape(height, width, 3)
+
+
+def render(scn, cam, image: np.ndarray, width: int, height: int, samples: int, num_subpixels: int = 2,
+           seed: int = DEFAULT_SEED, device: int = -1) -> np.ndarray:
+    """Drop-in for main.cpp:214-236: image (W*H RGB doubles, reference row
+    order, zero-initialised by the caller like main.cpp:210-212) receives
+    += sum_sub clamp(mean radiance) / num_subpixels^2 for every pixel."""
+    sp = _spheres_array(scn)
+    ca = _camera_array(cam)
+    img = image if image.dtype == np.float64 and image.flags["C_CONTIGUOUS"] else None
+    if img is None or img.size != width * height * 3:
+        raise ValueError("image must be a C-contiguous float64 array of width*height*3 values")
+    p = make_params(width, height, samples, num_subpixels, seed)
+    check(lib().ptg_render(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), C.byref(p),
+                           int(device), img.ctypes.data_as(C.c_void_p)), "ptg_render")
+    return image
+
+
+class Context:
+    """A scene prepared in HBM on one device (ptg_context)."""
+
+    def __init__(self, scn, cam, device: Optional[int] = None):
+        sp = _spheres_array(scn)
+        ca = _camera_array(cam)
+        h = C.c_void_p()
+        check(lib().ptg_context_create(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p),
+                                       -1 if device is None else int(device), C.byref(h)), "ptg_context_create")
+        self._h = h
+        self.n_spheres = len(sp)
+
+    def close(self):
+        if self._h:
+            lib().ptg_context_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def render_device(self, out, params: Params, segments=None, stream=None) -> None:
+        """Asynchronous render into `out` (torch float32 CUDA tensor of
+        shard_rows*W*3 values) on `stream` (torch.cuda.Stream or None =
+        torch's current stream)."""
+        import torch
+        _check_tensor(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
+                      * params.width * 3)
+        if segments is not None:
+            _check_tensor(segments, torch.int64, 1)
+        s = (stream or torch.cuda.current_stream(out.device)).cuda_stream
+        check(lib().ptg_render_device(self._h, C.byref(params), C.c_void_p(out.data_ptr()),
+                                      C.c_void_p(segments.data_ptr()) if segments is not None else None,
+                                      C.c_void_p(s)), "ptg_render_device")
+
+    def trace_samples(self, coords, params: Params):
+        """Parity probe: radiance + segment count of individual paths
+        (coords: int32 CUDA tensor [n, 5] = x, y, sx, sy, sample)."""
+        import torch
+        n = coords.shape[0]
+        out = torch.empty((n, 3), dtype=torch.float32, device=coords.device)
+        segs = torch.empty((n,), dtype=torch.int32, device=coords.device)
+        coords = coords.contiguous()
+        s = torch.cuda.current_stream(coords.device).cuda_stream
+        check(lib().ptg_trace_samples_device(self._h, C.byref(params), C.c_void_p(coords.data_ptr()), n,
+                                             C.c_void_p(out.data_ptr()), C.c_void_p(segs.data_ptr()),
+                                             C.c_void_p(s)), "ptg_trace_samples_device")
+        return out, segs
+
+
+def _check_tensor(t, dtype, min_numel):
+    if not t.is_cuda or t.dtype != dtype or not t.is_contiguous() or t.numel() < min_numel:
+        raise ValueError(f"expected a contiguous CUDA {dtype} tensor with >= {min_numel} elements")
+
+
+def unshard_device(gathered, image, width, height, band_rows, shard_count, stream=None):
+    import torch
+    s = (stream or torch.cuda.current_stream(image.device)).cuda_stream
+    check(lib().ptg_unshard_device(C.c_void_p(gathered.data_ptr()), C.c_void_p(image.data_ptr()), width, height,
+                                   band_rows, shard_count, C.c_void_p(s)), "ptg_unshard_device")
+
+
+def tonemap_device(image, out_u8, stream=None):
+    """utils.cpp:11-16 on the GPU: uint8 gamma-2.2 values of every channel."""
+    import torch
+    s = (stream or torch.cuda.current_stream(image.device)).cuda_stream
+    check(lib().ptg_tonemap_device(C.c_void_p(image.data_ptr()), C.c_void_p(out_u8.data_ptr()), image.numel(),
+                                   C.c_void_p(s)), "ptg_tonemap_device")
+
+
+def render_sharded(params: Params, slab, group=None,
+                   tile_renderer: Optional[Callable] = None, ctx: Optional[Context] = None,
+                   unshard: Optional[Callable] = None):
+    """One rank's part of a tile-sharded frame.
+
+    Renders this rank's bands into `slab`, then ONE gather collects every
+    slab on rank 0 (torch.distributed: RCCL over xGMI on the nccl backend,
+    gloo on CPU).  Rank 0 returns the reassembled image tensor [H, W, 3];
+    other ranks return None.  `tile_renderer(slab, params)` defaults to the
+    HIP megakernel (ctx.render_device); tests substitute a CPU renderer to
+    exercise the sharding logic with gloo."""
+    import torch
+    import torch.distributed as dist
+    if tile_renderer is None:
+        if ctx is None:
+            raise ValueError("render_sharded needs ctx (HIP path) or tile_renderer")
+        tile_renderer = lambda out, p: ctx.render_device(out, p)  # noqa: E731
+    tile_renderer(slab, params)
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    assert params.shard_count == world and params.shard_rank == rank
+    if rank == 0:
+        gathered = torch.empty((world,) + tuple(slab.shape), dtype=slab.dtype, device=slab.device)
+        dist.gather(slab, gather_list=list(gathered.unbind(0)), dst=0, group=group)
+        image = torch.empty((params.height, params.width, 3), dtype=slab.dtype, device=slab.device)
+        if unshard is not None:
+            unshard(gathered, image, params)
+        elif slab.is_cuda:
+            unshard_device(gathered, image, params.width, params.height, params.band_rows, world)
+        else:
+            image.copy_(torch.from_numpy(unshard_host(gathered.numpy(), params.width, params.height,
+                                                       params.band_rows, world)))
+        return image
+    dist.gather(slab, gather_list=None, dst=0, group=group)
+    return None

@@ -1,0 +1,140 @@
+/*
+ * ptgpu.h -- C ABI of the MI355X render loop (libptgpu.so).
+ *
+ * Drop-in for the per-pixel hot path of AlexandruIca/cpu-path-tracing:
+ * the taskflow row loop src/main.cpp:214-236 and everything it calls
+ * (render_subpixel main.cpp:179-197, radiance main.cpp:104-158, the scene scan
+ * main.cpp:30-42, the BRDF samplers main.cpp:44-97, camera::get_ray
+ * camera.cpp:32-38, sphere::intersect sphere.cpp:6-30, get_hit_record_at
+ * hit_record.cpp:3-12, rand_state random_state.cpp:3-17) runs as one HIP
+ * megakernel on gfx950.  Plain C types only: pointers, sizes, PODs.
+ *
+ * Conventions (reference: everything noexcept, no error codes):
+ *   every entry point returns PTG_OK (0) or a negative ptg_status and never
+ *   throws; ptg_last_error() returns a thread-local description of the last
+ *   failure.  Calls are not re-entrant on one context.
+ */
+#ifndef PTGPU_H
+#define PTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTG_ABI_VERSION 1
+
+typedef enum ptg_status {
+    PTG_OK = 0,
+    PTG_ERR_INVALID_ARGUMENT = -1,
+    PTG_ERR_HIP = -2,
+    PTG_ERR_NO_DEVICE = -3,
+    PTG_ERR_UNSUPPORTED = -4,
+    PTG_ERR_OUT_OF_MEMORY = -5
+} ptg_status;
+
+/* reflection.hpp:7-12 */
+typedef enum ptg_material { PTG_DIFFUSE = 0, PTG_SPECULAR = 1, PTG_DIELECTRIC = 2 } ptg_material;
+
+/* Field-for-field mirror of pt::sphere (sphere.hpp:10-17): 88 bytes, so a
+ * std::vector<pt::sphere>::data() can be passed as-is. */
+typedef struct ptg_sphere {
+    double radius;
+    double position[3];
+    double emission[3];
+    double color[3];
+    int32_t material; /* ptg_material (pt::reflection_type) */
+    int32_t reserved_;
+} ptg_sphere;
+
+/* Field-for-field mirror of pt::camera (camera.hpp:23-33): 176 bytes, the
+ * output of pt::camera::with_config (camera.cpp:3-17). */
+typedef struct ptg_camera {
+    double position[3];
+    double lower_left_corner[3];
+    double cam_x_axis[3];
+    double cam_y_axis[3];
+    double u[3];
+    double v[3];
+    double w[3];
+    double lens_radius;
+} ptg_camera;
+
+/* The ints main.cpp:202-206 hands to the loop, plus the counter-RNG seed
+ * (replacing std::random_device, random_state.cpp:5), the row-band shard and
+ * the work-unit size.
+ *
+ * Sample accumulation (main.cpp:192 `r = r + c * (1/samps)`, sequential
+ * double) is restated order-independently: every path's radiance is
+ * quantised to a u64 fixed-point value q(c) = trunc(c * 2^32) (c clamped to
+ * [0, 2^30]) and summed exactly; the sub-pixel mean is
+ * (float)((double)sum * 2^-32 / samps).  The image therefore does not depend
+ * on scheduling, chunking or sharding. */
+typedef struct ptg_params {
+    int32_t width;          /* main.cpp:204 */
+    int32_t height;         /* main.cpp:205 */
+    int32_t samples;        /* per sub-pixel (main.cpp:206: spp / num_subpixels^2) */
+    int32_t num_subpixels;  /* per axis (main.cpp:202); 1..8 */
+    uint64_t seed;          /* counter RNG key; the image does not depend on sharding */
+    int32_t band_rows;      /* shard: output rows per band (>= 1) */
+    int32_t shard_rank;     /* this shard renders bands b with b % shard_count == shard_rank */
+    int32_t shard_count;    /* 1 = whole image */
+    int32_t chunk_samples;  /* samples per sub-pixel per work unit (0 = auto); results do not depend on it */
+    int32_t flags;          /* reserved, 0 */
+} ptg_params;
+
+typedef struct ptg_context ptg_context;
+
+/* ---- metadata -------------------------------------------------------- */
+int ptg_abi_version(void);
+const char *ptg_last_error(void);
+int ptg_device_count(int *count);
+
+/* ---- drop-in entry point ---------------------------------------------
+ * Replaces main.cpp:214-236.  Synchronous.  image_rgb is the caller-owned
+ * std::vector<pt::vec3> viewed as width*height*3 doubles in the reference's
+ * row order (row (H-1-y)*W + x, main.cpp:181); like the loop, the call ADDS
+ * sum_sub clamp(mean)/num_subpixels^2 (main.cpp:195-196) into it.  With
+ * shard_count > 1 only the shard's bands are added.  device = -1: current. */
+int ptg_render(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam,
+               const ptg_params *params, int device, double *image_rgb);
+
+/* ---- device-resident path (bench, multi-GPU) --------------------------
+ * A context holds the prepared scene in HBM on one device. */
+int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int device,
+                       ptg_context **out);
+int ptg_context_destroy(ptg_context *ctx);
+
+/* Rows in one shard's slab: ceil(bands / shard_count) * band_rows. */
+int ptg_shard_rows(int32_t height, int32_t band_rows, int32_t shard_count, int32_t *rows);
+
+/* Asynchronous render on `stream` (hipStream_t; NULL = default stream).
+ * d_slab: device buffer of ptg_shard_rows(...) * width * 3 floats; slab row j
+ * holds output row ((j / band_rows) * shard_count + shard_rank) * band_rows +
+ * j % band_rows (rows >= height are left untouched).  Pixel values are
+ * written (not accumulated).  d_segments: optional device uint64 that
+ * receives += the number of scene scans (radiance segments) executed. */
+int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
+                      unsigned long long *d_segments, void *stream);
+
+/* Reassemble shard_count gathered slabs (rank-major, as all-gather lays them
+ * out) into the width*height*3 image. */
+int ptg_unshard_device(const float *d_gathered, float *d_image, int32_t width, int32_t height,
+                       int32_t band_rows, int32_t shard_count, void *stream);
+
+/* Output stage (utils.cpp:11-16 + main.cpp:240-247): 8-bit gamma-1/2.2
+ * values round(pow(clamp(x), 1/2.2) * 255) of `count` floats. */
+int ptg_tonemap_device(const float *d_image, uint8_t *d_out, size_t count, void *stream);
+
+/* Parity probe: trace individual samples.  d_coords holds n records
+ * {x, y, sx, sy, sample} (int32 each); d_out n*3 floats (radiance of that
+ * one path, main.cpp:191); d_segs n int32 (scene scans of that path). */
+int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const int32_t *d_coords, size_t n,
+                             float *d_out, int32_t *d_segs, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTGPU_H */

@@ -1,0 +1,975 @@
+/*
+ * pt_oracle.c -- TEST INFRASTRUCTURE ONLY: the CPU parity oracle and the
+ * timed CPU baseline ("port", the repo's own OpenMP loop).  See pt_oracle.h
+ * for the modes and the pinning status.  Never linked into the product.
+ *
+ * Every function cites the reference file:line it restates
+ * (AlexandruIca/cpu-path-tracing, /root/reference/src).  Build flags:
+ * -ffp-contract=off so that double arithmetic is evaluated exactly as the
+ * reference's out-of-line vec3 operators evaluate it (vec.cpp:15-69), and so
+ * that Mode B's float sequence only fuses where fmaf() is written.
+ */
+#include "pt_oracle.h"
+
+#include <math.h>
+#include <string.h>
+#include <stdlib.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define PO_EPS 1e-4      /* constants.hpp:7 */
+#define PO_PI 3.14159265358979323846 /* constants.hpp:8 */
+#define PO_INF 1e20      /* constants.hpp:9 */
+#define PO_DEPTH_LIMIT 100 /* constants.hpp:10 */
+#define PO_RR_THRESHOLD 4  /* main.cpp:106 */
+
+/* ========================================================================= */
+/* std::mt19937 (libstdc++ bits/random.tcc) + generate_canonical<double,53>   */
+/* ========================================================================= */
+void po_mt_seed(po_mt19937 *g, uint32_t seed)
+{
+    g->mt[0] = seed;
+    for (int i = 1; i < 624; ++i) {
+        uint32_t x = g->mt[i - 1];
+        g->mt[i] = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+    }
+    g->idx = 624;
+}
+
+static void po_mt_twist(po_mt19937 *g)
+{
+    const uint32_t upper = 0x80000000u, lower = 0x7fffffffu;
+    for (int k = 0; k < 624; ++k) {
+        uint32_t y = (g->mt[k] & upper) | (g->mt[(k + 1) % 624] & lower);
+        g->mt[k] = g->mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    g->idx = 0;
+}
+
+uint32_t po_mt_next(po_mt19937 *g)
+{
+    if (g->idx >= 624)
+        po_mt_twist(g);
+    uint32_t z = g->mt[g->idx++];
+    z ^= (z >> 11) & 0xffffffffu;
+    z ^= (z << 7) & 0x9d2c5680u;
+    z ^= (z << 15) & 0xefc60000u;
+    z ^= (z >> 18);
+    return z;
+}
+
+/* random_state.cpp:9-12 -> uniform_real_distribution<double>{0,1}(mt19937):
+ * generate_canonical<double,53> (random.tcc:3348-3380) draws two 32-bit words:
+ * (g0 + g1*2^32) / 2^64, clamped below 1; then *(1-0)+0. */
+double po_mt_generate(po_mt19937 *g)
+{
+    double sum = 0.0, tmp = 1.0;
+    for (int k = 0; k < 2; ++k) {
+        sum += (double)po_mt_next(g) * tmp;
+        tmp *= 4294967296.0;
+    }
+    double ret = sum / tmp;
+    if (ret >= 1.0)
+        ret = nextafter(1.0, 0.0);
+    return ret * (1.0 - 0.0) + 0.0;
+}
+
+/* random_state.cpp:14-17 */
+double po_mt_generate_between(po_mt19937 *g, double lo, double hi)
+{
+    return lo + (hi - lo) * po_mt_generate(g);
+}
+
+/* ========================================================================= */
+/* Counter-based xorshift (replaces pt::rand_state on the hot path)           */
+/* ========================================================================= */
+static uint64_t po_mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* key = mix64(seed ^ mix64(pixel_sub + 1)), pixel_sub = (y*W + x)*nsub^2 + sub */
+uint64_t po_key_hash(uint64_t seed, uint64_t pixel_sub)
+{
+    return po_mix64(seed ^ po_mix64(pixel_sub + 1ull));
+}
+
+/* per-sample xorshift32 state: high word of mix64(key + (s+1)*golden), never 0 */
+uint32_t po_sample_state(uint64_t key, uint32_t sample)
+{
+    uint32_t st = (uint32_t)(po_mix64(key + ((uint64_t)sample + 1ull) * 0x9E3779B97F4A7C15ull) >> 32);
+    return st ? st : 0x6D2B79F5u;
+}
+
+uint32_t po_xorshift32(uint32_t *state)
+{
+    uint32_t x = *state;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    *state = x;
+    return x;
+}
+
+/* one U[0,1) draw: top 24 bits, exact in float and in double */
+static float po_xs_f32(uint32_t *st) { return (float)(po_xorshift32(st) >> 8) * 0x1p-24f; }
+static double po_xs_f64(uint32_t *st) { return (double)(po_xorshift32(st) >> 8) * 0x1p-24; }
+
+/* ========================================================================= */
+/* Mode A: double vec3 with the reference's evaluation order (vec.cpp)        */
+/* ========================================================================= */
+typedef struct { double x, y, z; } v3;
+static v3 mk(double x, double y, double z) { v3 r = {x, y, z}; return r; }
+static v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }  /* vec.cpp:15-18 */
+static v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }  /* vec.cpp:20-23 */
+static v3 vmul(v3 a, double b) { return mk(a.x * b, a.y * b, a.z * b); }    /* vec.cpp:25-28 */
+static v3 vblend(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); } /* vec.cpp:30-33 */
+static double vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* vec.cpp:40-43 */
+static v3 vnorm(v3 a) { return vmul(a, 1 / sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); } /* vec.cpp:35-38 */
+static v3 vcross(v3 a, v3 b)                                                   /* vec.cpp:45-48 */
+{
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static v3 ld3(const double *p) { return mk(p[0], p[1], p[2]); }
+static void st3(double *p, v3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+
+/* vec.cpp:66-69 -> std::hypot(x,y,z) as libstdc++-11 __hypot3 implements it */
+double po_vec_length(const double v[3])
+{
+    double x = fabs(v[0]), y = fabs(v[1]), z = fabs(v[2]);
+    double a = x < y ? (y < z ? z : y) : (x < z ? z : x);
+    if (a != 0.0)
+        return a * sqrt((x / a) * (x / a) + (y / a) * (y / a) + (z / a) * (z / a));
+    return 0.0;
+}
+
+/* utils.cpp:6-9 (std::clamp(x, 0, 1)) */
+double po_clamp(double x) { return x < 0.0 ? 0.0 : (1.0 < x ? 1.0 : x); }
+
+/* utils.cpp:11-16 */
+int po_color_to_int(double x) { return (int)round(pow(po_clamp(x), 1.0 / 2.2) * 255.0); }
+
+void po_tonemap(const double *image, size_t count, int32_t *out)
+{
+    for (size_t i = 0; i < count; ++i)
+        out[i] = po_color_to_int(image[i]);
+}
+
+/* camera.cpp:3-17 */
+void po_camera_with_config(const po_camera_config *cfg, po_camera *out)
+{
+    double vh = 2.0 * tan(0.5 * cfg->vertical_fov_radians);
+    double vw = cfg->aspect_ratio * vh;
+    v3 pos = ld3(cfg->position);
+    v3 w = vnorm(vsub(pos, ld3(cfg->direction)));
+    v3 u = vnorm(vcross(ld3(cfg->up), w));
+    v3 v = vcross(w, u);
+    v3 X = vmul(vmul(u, vw), cfg->focus_distance);
+    v3 Y = vmul(vmul(v, vh), cfg->focus_distance);
+    v3 llc = vsub(vsub(vsub(pos, vmul(X, 0.5)), vmul(Y, 0.5)), vmul(w, cfg->focus_distance));
+    st3(out->position, pos);
+    st3(out->lower_left_corner, llc);
+    st3(out->cam_x_axis, X);
+    st3(out->cam_y_axis, Y);
+    st3(out->u, u);
+    st3(out->v, v);
+    st3(out->w, w);
+    out->lens_radius = cfg->aperture / 2.0;
+}
+
+/* A generic draw source for Mode A: the reference's mt19937 or the counter RNG */
+typedef struct {
+    po_mt19937 *mt;
+    uint32_t xs;
+    int draws;
+} rngA;
+
+static double drawA(rngA *r)
+{
+    r->draws++;
+    return r->mt ? po_mt_generate(r->mt) : po_xs_f64(&r->xs);
+}
+static double drawA_between(rngA *r, double lo, double hi) { return lo + (hi - lo) * drawA(r); }
+
+/* camera.cpp:19-30 + camera.cpp:32-38 */
+static void cam_get_ray_A(const po_camera *cam, double s, double t, rngA *r, v3 *ro, v3 *rd)
+{
+    v3 p;
+    for (;;) {
+        double px = drawA_between(r, -1.0, 1.0);
+        double py = drawA_between(r, -1.0, 1.0);
+        p = mk(px, py, 0.0);
+        if (vdot(p, p) >= 1.0)
+            continue;
+        break;
+    }
+    v3 rdisk = vmul(p, cam->lens_radius);
+    v3 off = vadd(vmul(rdisk, s), vmul(rdisk, t)); /* camera.cpp:35 quirk: rd*s + rd*t */
+    v3 dir = vsub(vsub(vadd(vadd(ld3(cam->lower_left_corner), vmul(ld3(cam->cam_x_axis), s)),
+                            vmul(ld3(cam->cam_y_axis), t)),
+                       ld3(cam->position)),
+                  off);
+    *ro = vadd(ld3(cam->position), off);
+    *rd = dir;
+}
+
+int po_camera_get_ray_mt(const po_camera *cam, double s, double t, po_mt19937 *g, double origin[3],
+                         double direction[3])
+{
+    rngA r = {g, 0, 0};
+    v3 o, d;
+    cam_get_ray_A(cam, s, t, &r, &o, &d);
+    st3(origin, o);
+    st3(direction, d);
+    return r.draws;
+}
+
+/* sphere.cpp:6-30 */
+static double sphere_intersect_A(const po_sphere *sp, v3 o, v3 d)
+{
+    v3 oc = vsub(o, ld3(sp->position));
+    double a = vdot(d, d);
+    double hb = vdot(oc, d);
+    double c = vdot(oc, oc) - sp->radius * sp->radius;
+    double disc = hb * hb - a * c;
+    if (disc < 0)
+        return 0.0;
+    double sq = sqrt(disc);
+    double root = (-hb - sq) / a;
+    if (root < PO_EPS) {
+        root = (-hb + sq) / a;
+        if (root < PO_EPS)
+            return 0.0;
+    }
+    return root;
+}
+
+double po_sphere_intersect(const po_sphere *sp, const double origin[3], const double direction[3])
+{
+    return sphere_intersect_A(sp, ld3(origin), ld3(direction));
+}
+
+/* main.cpp:30-42 (strict < keeps the lowest index on ties) */
+static int intersect_A(const po_sphere *s, int n, v3 o, v3 d, double *t, int *id)
+{
+    *t = PO_INF;
+    for (int i = 0; i < n; ++i) {
+        double dd = sphere_intersect_A(&s[i], o, d);
+        if (dd > 0 && dd < *t) {
+            *t = dd;
+            *id = i;
+        }
+    }
+    return *t < PO_INF;
+}
+
+int po_intersect_scene(const po_sphere *s, int n, const double o[3], const double d[3], double *t, int *id)
+{
+    *id = -1;
+    return intersect_A(s, n, ld3(o), ld3(d), t, id);
+}
+
+/* hit_record.cpp:3-12 */
+typedef struct {
+    v3 o, d;   /* original ray */
+    v3 p, on, n;
+    int front;
+} recA;
+
+static recA hit_record_A(const po_sphere *sp, v3 o, v3 d, double t)
+{
+    recA r;
+    r.o = o;
+    r.d = d;
+    r.p = vadd(o, vmul(d, t)); /* ray.cpp:3-6 */
+    r.on = vnorm(vsub(r.p, ld3(sp->position)));
+    r.front = vdot(r.on, d) < 0;
+    r.n = r.front ? r.on : vmul(r.on, -1);
+    return r;
+}
+
+void po_hit_record(const po_sphere *sp, const double origin[3], const double direction[3], double t,
+                   double out[10])
+{
+    recA r = hit_record_A(sp, ld3(origin), ld3(direction), t);
+    st3(out, r.p);
+    st3(out + 3, r.on);
+    st3(out + 6, r.n);
+    out[9] = r.front;
+}
+
+static recA rec_from(const double rec[10], const double o[3], const double d[3])
+{
+    recA r;
+    r.o = ld3(o);
+    r.d = ld3(d);
+    r.p = ld3(rec);
+    r.on = ld3(rec + 3);
+    r.n = ld3(rec + 6);
+    r.front = rec[9] != 0.0;
+    return r;
+}
+
+/* main.cpp:44-58 */
+static void diffuse_A(const recA *rec, rngA *r, v3 *ro, v3 *rd)
+{
+    double phi = 2 * PO_PI * drawA(r);
+    double ra = drawA(r);
+    double st = sqrt(ra);
+    double ct = sqrt(1.0 - ra);
+    v3 w = rec->n;
+    v3 u = vnorm(vcross(fabs(w.x) > 0.1 ? mk(0, 1, 0) : mk(1, 0, 0), w));
+    v3 v = vcross(w, u);
+    v3 nd = vnorm(vadd(vadd(vmul(vmul(u, cos(phi)), st), vmul(vmul(v, sin(phi)), st)), vmul(w, ct)));
+    *ro = rec->p;
+    *rd = nd;
+}
+
+/* main.cpp:60-67 */
+static void specular_A(const recA *rec, rngA *r, v3 *ro, v3 *rd)
+{
+    const double fuzziness = 0.0;
+    v3 refl = vsub(rec->d, vmul(vmul(rec->on, 2.0), vdot(rec->on, rec->d)));
+    double f = drawA(r) * fuzziness;
+    *ro = rec->p;
+    *rd = vadd(refl, mk(f, f, f));
+}
+
+/* main.cpp:82-87 */
+static double reflectance_A(double cosine, double ref_idx)
+{
+    double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
+    r0 *= r0;
+    return r0 + (1.0 - r0) * pow(1.0 - cosine, 5);
+}
+
+/* main.cpp:69-97 */
+static void dielectric_A(const recA *rec, rngA *r, v3 *ro, v3 *rd)
+{
+    const double refraction_index = 2.0;
+    double ratio = rec->front ? (1.0 / refraction_index) : refraction_index;
+    v3 ud = vnorm(rec->d);
+    double x = vdot(vmul(ud, -1.0), rec->n);
+    double ct = 1.0 < x ? 1.0 : x; /* std::min(x, 1.0) */
+    double st = sqrt(1.0 - ct * ct);
+    int cannot = ratio * st > 1.0;
+    if (cannot || reflectance_A(ct, ratio) > drawA(r)) { /* short-circuit: no draw on TIR */
+        specular_A(rec, r, ro, rd);
+        return;
+    }
+    v3 perp = vmul(vadd(ud, vmul(rec->n, ct)), ratio);
+    v3 par = vmul(rec->n, -sqrt(fabs(1.0 - vdot(perp, perp))));
+    *ro = rec->p;
+    *rd = vadd(perp, par);
+}
+
+#define BRDF_WRAPPER(name, fn)                                                                     \
+    int name(const double rec[10], const double o[3], const double d[3], po_mt19937 *g, double ro[3], \
+             double rd[3])                                                                         \
+    {                                                                                              \
+        rngA r = {g, 0, 0};                                                                        \
+        recA h = rec_from(rec, o, d);                                                              \
+        v3 a, b;                                                                                   \
+        fn(&h, &r, &a, &b);                                                                        \
+        st3(ro, a);                                                                                \
+        st3(rd, b);                                                                                \
+        return r.draws;                                                                            \
+    }
+BRDF_WRAPPER(po_diffuse_ray_mt, diffuse_A)
+BRDF_WRAPPER(po_specular_ray_mt, specular_A)
+BRDF_WRAPPER(po_dielectric_ray_mt, dielectric_A)
+
+/* main.cpp:104-158; *segs = number of scene scans */
+static v3 radiance_A(const po_sphere *s, int n, v3 o, v3 d, rngA *r, int *segs)
+{
+    v3 E = mk(0, 0, 0), T = mk(1, 1, 1);
+    *segs = 0;
+    for (int depth = 0; depth < PO_DEPTH_LIMIT; ++depth) {
+        double t = 0.0;
+        int id = 0;
+        (*segs)++;
+        if (!intersect_A(s, n, o, d, &t, &id)) {
+            v3 ud = vnorm(d);
+            double tt = 0.5 * (ud.y + 1.0);
+            v3 bg = vadd(vmul(mk(1, 1, 1), 1.0 - tt), vmul(mk(0.5, 0.7, 1.0), tt));
+            return vadd(E, vblend(T, bg));
+        }
+        const po_sphere *obj = &s[id];
+        recA rec = hit_record_A(obj, o, d, t);
+        v3 color = ld3(obj->color);
+        E = vadd(E, vblend(T, ld3(obj->emission)));
+        double p = color.x;
+        if (p < color.y) p = color.y;
+        if (p < color.z) p = color.z; /* std::max({x,y,z}) */
+        if (depth > PO_RR_THRESHOLD) {
+            if (drawA(r) < p)
+                color = vmul(color, 1.0 / p);
+            else
+                return E;
+        }
+        T = vblend(T, color);
+        switch (obj->material) {
+        case 0: diffuse_A(&rec, r, &o, &d); break;
+        case 1: specular_A(&rec, r, &o, &d); break;
+        default: dielectric_A(&rec, r, &o, &d); break;
+        }
+    }
+    return E;
+}
+
+int po_radiance_mt(const po_sphere *s, int n, const double o[3], const double d[3], po_mt19937 *g, double out[3])
+{
+    rngA r = {g, 0, 0};
+    int segs = 0;
+    v3 c = radiance_A(s, n, ld3(o), ld3(d), &r, &segs);
+    st3(out, c);
+    return segs;
+}
+
+/* main.cpp:179-197 for one sub-pixel; *r supplies the draws */
+static v3 subpixel_A(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub, int x,
+                     int y, int sx, int sy, rngA *r, uint64_t key, uint64_t *segs)
+{
+    v3 acc = mk(0, 0, 0);
+    for (int k = 0; k < samps; ++k) {
+        if (!r->mt)
+            r->xs = po_sample_state(key, (uint32_t)k);
+        double sl = 1.0 / nsub;
+        double xin = (x + sx * sl + drawA_between(r, 0.0, sl));
+        double yin = (y + sy * sl + drawA_between(r, 0.0, sl));
+        v3 o, d;
+        cam_get_ray_A(cam, xin / W, yin / H, r, &o, &d);
+        int sg = 0;
+        v3 c = radiance_A(s, n, o, d, r, &sg);
+        *segs += (uint64_t)sg;
+        acc = vadd(acc, vmul(c, 1.0 / samps));
+    }
+    return acc;
+}
+
+static int check_args(int n, int W, int H, int samps, int nsub)
+{
+    return n < 0 || W <= 0 || H <= 0 || samps < 0 || nsub <= 0;
+}
+
+/* main.cpp:214-236 with the reference's row seeding (main.cpp:222-223) */
+int po_render_mt(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                 uint32_t rd_value, int y0, int y1, int ystep, int nthreads, double *image)
+{
+    if (check_args(n, W, H, samps, nsub) || ystep <= 0)
+        return -1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int y = y0; y < y1; y += ystep) {
+        unsigned short seed = (unsigned short)(y * y * y);
+        po_mt19937 g;
+        po_mt_seed(&g, rd_value * (uint32_t)seed);
+        rngA r = {&g, 0, 0};
+        uint64_t segs = 0;
+        for (int x = 0; x < W; ++x)
+            for (int sy = 0; sy < nsub; ++sy)
+                for (int sx = 0; sx < nsub; ++sx) {
+                    v3 a = subpixel_A(s, n, cam, W, H, samps, nsub, x, y, sx, sy, &r, 0, &segs);
+                    size_t row = (size_t)(H - y - 1) * (size_t)W + (size_t)x;
+                    double *px = image + 3 * row;
+                    double q = 1.0 / (nsub * nsub);
+                    px[0] = px[0] + po_clamp(a.x) * q;
+                    px[1] = px[1] + po_clamp(a.y) * q;
+                    px[2] = px[2] + po_clamp(a.z) * q;
+                }
+    }
+    return 0;
+}
+
+int po_render_xs_f64(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                     uint64_t seed, int y0, int y1, int ystep, int nthreads, double *image, uint64_t *segments)
+{
+    if (check_args(n, W, H, samps, nsub) || ystep <= 0)
+        return -1;
+    uint64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+    for (int y = y0; y < y1; y += ystep) {
+        for (int x = 0; x < W; ++x)
+            for (int sy = 0; sy < nsub; ++sy)
+                for (int sx = 0; sx < nsub; ++sx) {
+                    uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) +
+                                  (uint64_t)(sy * nsub + sx);
+                    rngA r = {NULL, 0, 0};
+                    uint64_t segs = 0;
+                    v3 a = subpixel_A(s, n, cam, W, H, samps, nsub, x, y, sx, sy, &r, po_key_hash(seed, ps),
+                                      &segs);
+                    total += segs;
+                    size_t row = (size_t)(H - y - 1) * (size_t)W + (size_t)x;
+                    double *px = image + 3 * row;
+                    double q = 1.0 / (nsub * nsub);
+                    px[0] = px[0] + po_clamp(a.x) * q;
+                    px[1] = px[1] + po_clamp(a.y) * q;
+                    px[2] = px[2] + po_clamp(a.z) * q;
+                }
+    }
+    if (segments)
+        *segments = total;
+    return 0;
+}
+
+/* ========================================================================= */
+/* Mode B: the float op sequence of the GPU megakernel (DESIGN.md "Mode B")   */
+/* ========================================================================= */
+#define BIG_RADIUS 1000.0
+#define EPSF 1e-4f
+#define INFF 1e20f
+
+typedef struct { float x, y, z; } f3;
+static f3 fk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static float fdot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static f3 fnorm(f3 a)
+{
+    float inv = 1.0f / sqrtf(fdot(a, a));
+    return fk(a.x * inv, a.y * inv, a.z * inv);
+}
+static f3 fcross(f3 a, f3 b)
+{
+    return fk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+
+typedef struct {
+    f3 P, N;          /* anchor point and anchor normal (big) or centre and 0 */
+    float R, R2x, negR2;
+    int big;
+    f3 C;             /* centre (float) for normals */
+    f3 emis, col, col_rr;
+    float prob;
+    int mat;
+} sphB;
+
+typedef struct {
+    f3 pos, base, X, Y; /* base = float(llc - pos) */
+    float lens;
+} camB;
+
+static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
+{
+    for (int i = 0; i < n; ++i) {
+        const po_sphere *sp = &s[i];
+        sphB *b = &out[i];
+        double R = sp->radius;
+        b->big = R >= BIG_RADIUS;
+        b->R = (float)R;
+        b->R2x = (float)(2.0 * R);
+        b->negR2 = (float)(-(R * R));
+        if (b->big) {
+            double vx = cam->position[0] - sp->position[0];
+            double vy = cam->position[1] - sp->position[1];
+            double vz = cam->position[2] - sp->position[2];
+            double len = sqrt(vx * vx + vy * vy + vz * vz);
+            double nx = 0.0, ny = 1.0, nz = 0.0;
+            if (len > 0.0) {
+                nx = vx / len;
+                ny = vy / len;
+                nz = vz / len;
+            }
+            b->P = fk((float)(sp->position[0] + R * nx), (float)(sp->position[1] + R * ny),
+                      (float)(sp->position[2] + R * nz));
+            b->N = fk((float)nx, (float)ny, (float)nz);
+        } else {
+            b->P = fk((float)sp->position[0], (float)sp->position[1], (float)sp->position[2]);
+            b->N = fk(0.0f, 0.0f, 0.0f);
+        }
+        b->C = fk((float)sp->position[0], (float)sp->position[1], (float)sp->position[2]);
+        b->emis = fk((float)sp->emission[0], (float)sp->emission[1], (float)sp->emission[2]);
+        b->col = fk((float)sp->color[0], (float)sp->color[1], (float)sp->color[2]);
+        float p = b->col.x;
+        if (p < b->col.y) p = b->col.y;
+        if (p < b->col.z) p = b->col.z;
+        b->prob = p;
+        if (p > 0.0f) {
+            float inv = 1.0f / p;
+            b->col_rr = fk(b->col.x * inv, b->col.y * inv, b->col.z * inv);
+        } else {
+            b->col_rr = fk(0.0f, 0.0f, 0.0f);
+        }
+        b->mat = sp->material;
+    }
+    cb->pos = fk((float)cam->position[0], (float)cam->position[1], (float)cam->position[2]);
+    cb->base = fk((float)(cam->lower_left_corner[0] - cam->position[0]),
+                  (float)(cam->lower_left_corner[1] - cam->position[1]),
+                  (float)(cam->lower_left_corner[2] - cam->position[2]));
+    cb->X = fk((float)cam->cam_x_axis[0], (float)cam->cam_x_axis[1], (float)cam->cam_x_axis[2]);
+    cb->Y = fk((float)cam->cam_y_axis[0], (float)cam->cam_y_axis[1], (float)cam->cam_y_axis[2]);
+    cb->lens = (float)cam->lens_radius;
+}
+
+/* sin/cos of 2*pi*u for u in [0,1): quadrant split of 4u (exact) and Taylor
+ * polynomials of sin(pi/2 f), cos(pi/2 f) on f in [0,1) (replaces libm in
+ * main.cpp:55 so host and device agree bit-for-bit). */
+static void sincos2pi_B(float u, float *c, float *s)
+{
+    float v = u * 4.0f;
+    float qf = floorf(v);
+    float f = v - qf;
+    int q = (int)qf & 3;
+    float f2 = f * f;
+    float ps = fmaf(f2, 0x1.e8f434p-25f, -0x1.e3075p-19f);
+    ps = fmaf(f2, ps, 0x1.507834p-13f);
+    ps = fmaf(f2, ps, -0x1.32d2ccp-8f);
+    ps = fmaf(f2, ps, 0x1.466bc6p-4f);
+    ps = fmaf(f2, ps, -0x1.4abbcep-1f);
+    ps = fmaf(f2, ps, 0x1.921fb6p+0f);
+    float sn = f * ps;
+    float pc = fmaf(f2, -0x1.b6e25p-28f, 0x1.f9d38ap-22f);
+    pc = fmaf(f2, pc, -0x1.a6d1f2p-16f);
+    pc = fmaf(f2, pc, 0x1.e1f506p-11f);
+    pc = fmaf(f2, pc, -0x1.55d3c8p-6f);
+    pc = fmaf(f2, pc, 0x1.03c1fp-2f);
+    pc = fmaf(f2, pc, -0x1.3bd3ccp+0f);
+    float cs = fmaf(f2, pc, 1.0f);
+    float rc = (q == 0) ? cs : (q == 1) ? -sn : (q == 2) ? -cs : sn;
+    float rs = (q == 0) ? sn : (q == 1) ? cs : (q == 2) ? -sn : -cs;
+    *c = rc;
+    *s = rs;
+}
+
+/* Scene scan, Mode B (main.cpp:30-42 + sphere.cpp:6-30 with the stable
+ * quadratic roots; huge spheres use the anchored form) */
+static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
+{
+    float a = fdot(d, d);
+    float tb = INFF;
+    int id = -1;
+    for (int i = 0; i < n; ++i) {
+        const sphB *sp = &s[i];
+        f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
+        float ed = fdot(e, d);
+        float ee = fdot(e, e);
+        float hb, c;
+        if (sp->big) {
+            hb = fmaf(sp->R, fdot(sp->N, d), ed);
+            c = fmaf(sp->R2x, fdot(e, sp->N), ee);
+        } else {
+            hb = ed;
+            c = ee + sp->negR2;
+        }
+        float disc = fmaf(hb, hb, -(a * c));
+        if (disc < 0.0f)
+            continue;
+        float sq = sqrtf(disc);
+        float q = -(hb + copysignf(sq, hb));
+        float t1 = q / a, t2 = c / q;
+        float tmin = t1 < t2 ? t1 : t2;
+        float tmax = t1 < t2 ? t2 : t1;
+        float root = tmin;
+        if (root < EPSF) {
+            root = tmax;
+            if (root < EPSF)
+                continue;
+        }
+        if (root > 0.0f && root < tb) {
+            tb = root;
+            id = i;
+        }
+    }
+    *tout = tb;
+    *idout = id;
+    return tb < INFF;
+}
+
+static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub, int x, int y, int sx, int sy,
+                   uint32_t st, int *segs)
+{
+    float sl = 1.0f / (float)nsub;
+    float u1 = po_xs_f32(&st);
+    float u2 = po_xs_f32(&st);
+    float xin = fmaf(sl, u1, (float)x + (float)sx * sl);
+    float yin = fmaf(sl, u2, (float)y + (float)sy * sl);
+    float fs = xin / (float)W, ft = yin / (float)H;
+    float px, py;
+    for (;;) {
+        px = fmaf(2.0f, po_xs_f32(&st), -1.0f);
+        py = fmaf(2.0f, po_xs_f32(&st), -1.0f);
+        if (fmaf(py, py, px * px) >= 1.0f)
+            continue;
+        break;
+    }
+    float sst = fs + ft;
+    float ox = (px * cam->lens) * sst, oy = (py * cam->lens) * sst;
+    f3 o = fk(cam->pos.x + ox, cam->pos.y + oy, cam->pos.z);
+    f3 d = fk(fmaf(cam->Y.x, ft, fmaf(cam->X.x, fs, cam->base.x)) - ox,
+              fmaf(cam->Y.y, ft, fmaf(cam->X.y, fs, cam->base.y)) - oy,
+              fmaf(cam->Y.z, ft, fmaf(cam->X.z, fs, cam->base.z)));
+    f3 E = fk(0, 0, 0), T = fk(1, 1, 1);
+    *segs = 0;
+    for (int depth = 0; depth < PO_DEPTH_LIMIT; ++depth) {
+        float t;
+        int id;
+        (*segs)++;
+        if (!intersect_B(s, n, o, d, &t, &id)) {
+            f3 ud = fnorm(d);
+            float tt = 0.5f * (ud.y + 1.0f);
+            float it = 1.0f - tt;
+            E = fk(fmaf(T.x, fmaf(tt, 0.5f, it), E.x), fmaf(T.y, fmaf(tt, 0.7f, it), E.y),
+                   fmaf(T.z, fmaf(tt, 1.0f, it), E.z));
+            return E;
+        }
+        const sphB *sp = &s[id];
+        f3 p = fk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z));
+        f3 on = fnorm(fk(p.x - sp->C.x, p.y - sp->C.y, p.z - sp->C.z));
+        int front = fdot(on, d) < 0.0f;
+        f3 nn = front ? on : fk(-on.x, -on.y, -on.z);
+        E = fk(fmaf(T.x, sp->emis.x, E.x), fmaf(T.y, sp->emis.y, E.y), fmaf(T.z, sp->emis.z, E.z));
+        f3 col = sp->col;
+        if (depth > PO_RR_THRESHOLD) {
+            if (po_xs_f32(&st) < sp->prob)
+                col = sp->col_rr;
+            else
+                return E;
+        }
+        T = fk(T.x * col.x, T.y * col.y, T.z * col.z);
+        int reflect = 0;
+        if (sp->mat == 0) { /* diffuse, main.cpp:44-58 */
+            float u_phi = po_xs_f32(&st);
+            float ra = po_xs_f32(&st);
+            float cp, sp_;
+            sincos2pi_B(u_phi, &cp, &sp_);
+            float sth = sqrtf(ra);
+            float cth = sqrtf(1.0f - ra);
+            f3 w = nn;
+            f3 uu = fabsf(w.x) > 0.1f ? fk(w.z, 0.0f, -w.x) : fk(0.0f, -w.z, w.y);
+            uu = fnorm(uu);
+            f3 vv = fcross(w, uu);
+            float cs = cp * sth, ss = sp_ * sth;
+            f3 nd = fk(fmaf(w.x, cth, fmaf(vv.x, ss, uu.x * cs)), fmaf(w.y, cth, fmaf(vv.y, ss, uu.y * cs)),
+                       fmaf(w.z, cth, fmaf(vv.z, ss, uu.z * cs)));
+            o = p;
+            d = fnorm(nd);
+            continue;
+        } else if (sp->mat == 2) { /* dielectric, main.cpp:69-97 */
+            float ratio = front ? 0.5f : 2.0f;
+            f3 ud = fnorm(d);
+            float x0 = -fdot(ud, nn);
+            float cth = 1.0f < x0 ? 1.0f : x0;
+            float sth = sqrtf(fmaf(-cth, cth, 1.0f));
+            int cannot = ratio * sth > 1.0f;
+            if (cannot) {
+                reflect = 1;
+            } else {
+                float r0 = (1.0f - ratio) / (1.0f + ratio);
+                r0 = r0 * r0;
+                float xm = 1.0f - cth;
+                float x2 = xm * xm;
+                float x5 = (x2 * x2) * xm;
+                float R = fmaf(1.0f - r0, x5, r0);
+                reflect = R > po_xs_f32(&st);
+            }
+            if (!reflect) {
+                f3 perp = fk(fmaf(nn.x, cth, ud.x) * ratio, fmaf(nn.y, cth, ud.y) * ratio,
+                             fmaf(nn.z, cth, ud.z) * ratio);
+                float sq = sqrtf(fabsf(1.0f - fdot(perp, perp)));
+                o = p;
+                d = fk(fmaf(nn.x, -sq, perp.x), fmaf(nn.y, -sq, perp.y), fmaf(nn.z, -sq, perp.z));
+                continue;
+            }
+        }
+        /* specular (main.cpp:60-67), also the dielectric's reflection */
+        {
+            float k = fdot(on, d);
+            k = k + k;
+            (void)po_xs_f32(&st); /* fuzz draw: consumed, times 0 */
+            o = p;
+            d = fk(fmaf(-k, on.x, d.x), fmaf(-k, on.y, d.y), fmaf(-k, on.z, d.z));
+        }
+    }
+    return E;
+}
+
+/* Exact, order-independent sample accumulation (include/ptgpu.h "Sample
+ * accumulation"): q(c) = trunc(c * 2^32), c clamped to [0, 2^30]; the
+ * sub-pixel mean is (float)((double)sum * 2^-32 / samps) (main.cpp:192). */
+static uint64_t quant_B(float c)
+{
+    if (!(c >= 0.0f))
+        return 0;
+    if (c > 0x1p30f)
+        c = 0x1p30f;
+    return (uint64_t)((double)c * 0x1p32);
+}
+
+static float mean_B(uint64_t sum, int samps)
+{
+    return samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)samps) : 0.0f;
+}
+
+static f3 subpixel_B(const sphB *s, int n, const camB *cam, int W, int H, int samps, int nsub, int x, int y,
+                     int sx, int sy, uint64_t key, uint64_t *segs)
+{
+    uint64_t ax = 0, ay = 0, az = 0;
+    for (int k = 0; k < samps; ++k) {
+        int sg = 0;
+        f3 c = sample_B(s, n, cam, W, H, nsub, x, y, sx, sy, po_sample_state(key, (uint32_t)k), &sg);
+        *segs += (uint64_t)sg;
+        ax += quant_B(c.x);
+        ay += quant_B(c.y);
+        az += quant_B(c.z);
+    }
+    return fk(mean_B(ax, samps), mean_B(ay, samps), mean_B(az, samps));
+}
+
+static float clampf_B(float v) { return v < 0.0f ? 0.0f : (1.0f < v ? 1.0f : v); }
+
+int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                     uint64_t seed, int y0, int y1, int ystep, int nthreads, float *image, uint64_t *segments)
+{
+    if (check_args(n, W, H, samps, nsub) || ystep <= 0)
+        return -1;
+    sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
+    camB cb;
+    prep_B(s, n, cam, sb, &cb);
+    uint64_t total = 0;
+    float q = 1.0f / (float)(nsub * nsub);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+    for (int y = y0; y < y1; y += ystep) {
+        for (int x = 0; x < W; ++x) {
+            f3 pix = fk(0, 0, 0);
+            for (int sy = 0; sy < nsub; ++sy)
+                for (int sx = 0; sx < nsub; ++sx) {
+                    uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) +
+                                  (uint64_t)(sy * nsub + sx);
+                    uint64_t segs = 0;
+                    f3 a = subpixel_B(sb, n, &cb, W, H, samps, nsub, x, y, sx, sy, po_key_hash(seed, ps), &segs);
+                    total += segs;
+                    pix = fk(fmaf(clampf_B(a.x), q, pix.x), fmaf(clampf_B(a.y), q, pix.y),
+                             fmaf(clampf_B(a.z), q, pix.z));
+                }
+            size_t row = (size_t)(H - y - 1) * (size_t)W + (size_t)x;
+            image[3 * row + 0] = pix.x;
+            image[3 * row + 1] = pix.y;
+            image[3 * row + 2] = pix.z;
+        }
+    }
+    free(sb);
+    if (segments)
+        *segments = total;
+    return 0;
+}
+
+int po_sample_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H, int nsub, uint64_t seed, int x,
+                  int y, int sx, int sy, uint32_t sample, float out[3])
+{
+    sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
+    camB cb;
+    prep_B(s, n, cam, sb, &cb);
+    uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) + (uint64_t)(sy * nsub + sx);
+    int segs = 0;
+    f3 c = sample_B(sb, n, &cb, W, H, nsub, x, y, sx, sy, po_sample_state(po_key_hash(seed, ps), sample), &segs);
+    out[0] = c.x;
+    out[1] = c.y;
+    out[2] = c.z;
+    free(sb);
+    return segs;
+}
+
+/* ========================================================================= */
+/* Scenes: values of simple_scene.hpp:18-49, box_scene.hpp:16-69,             */
+/* box_mirror_scene.hpp:16-69, computed with the same double expressions.     */
+/* ========================================================================= */
+static void put(po_sphere *s, double r, double px, double py, double pz, double ex, double ey, double ez, double cx,
+                double cy, double cz, int m)
+{
+    memset(s, 0, sizeof(*s));
+    s->radius = r;
+    s->position[0] = px; s->position[1] = py; s->position[2] = pz;
+    s->emission[0] = ex; s->emission[1] = ey; s->emission[2] = ez;
+    s->color[0] = cx; s->color[1] = cy; s->color[2] = cz;
+    s->material = m;
+}
+
+static void cfg_defaults(po_camera_config *c)
+{
+    memset(c, 0, sizeof(*c));
+    c->up[1] = 1.0;                      /* camera.hpp:15 */
+    c->aspect_ratio = 16.0 / 9.0;        /* camera.hpp:16 */
+    c->vertical_fov_radians = 0.785398163; /* camera.hpp:17 */
+    c->focal_length = 1.0;               /* camera.hpp:18 */
+}
+
+int po_scene(int id, int w, int h, po_sphere *out, int cap, po_camera_config *cfg)
+{
+    po_sphere tmp[8];
+    int n = 0;
+    cfg_defaults(cfg);
+    if (id == 0) { /* simple_scene.hpp:14-52 */
+        put(&tmp[n++], 100.0, 0.0, -100.5, -1.0, 0, 0, 0, 0.8, 0.8, 0.0, 0);
+        put(&tmp[n++], 0.5, 1.0, 0.0, -1.0, 0, 0, 0, 0.999, 0.999, 0.999, 1);
+        put(&tmp[n++], 0.5, -1.0, 0.0, -1.0, 0, 0, 0, 0.999, 0.999, 0.999, 2);
+        put(&tmp[n++], 0.5, 0.0, 0.0, -1.0, 0.1, 0.1, 0.9, 0.0, 0.7, 0.1, 0);
+        put(&tmp[n++], 1.0, 1.0, 3.1, -1.0, 30.0, 30.0, 30.0, 0.0, 0.0, 0.0, 0);
+        cfg->position[0] = -2.0; cfg->position[1] = 2.0; cfg->position[2] = 1.0;
+        cfg->direction[0] = 0.0; cfg->direction[1] = 0.0; cfg->direction[2] = -1.0;
+        cfg->vertical_fov_radians = 1.2;
+    } else if (id == 1 || id == 2) { /* box_scene.hpp:14-72 / box_mirror_scene.hpp:14-72 */
+        const double big = 1E6, off = 0.4, y = 0.0, z = -1.0;
+        int wall = id == 1 ? 0 : 1;
+        put(&tmp[n++], big, -big - off, y, z, 0, 0, 0, 0.9, 0.1, 0.2, wall);
+        put(&tmp[n++], big, big + off, y, z, 0, 0, 0, 0.3, 0.1, 0.9, wall);
+        put(&tmp[n++], big, 0.0, 0.0, z - big, 0, 0, 0, 0.1, 0.7, 0.2, wall);
+        put(&tmp[n++], big, 0.0, big + off, z, 0, 0, 0, 0.3, 0.7, 0.2, wall);
+        put(&tmp[n++], big, 0.0, -big - off, z, 0, 0, 0, 0.9, 0.9, 0.9, wall);
+        if (id == 1) {
+            put(&tmp[n++], off / 2.0, 0.0, 0.0 + off / 4.0, z - off / 2.5, 9.0, 9.0, 9.0, 1.8, 1.8, 1.8, 0);
+            put(&tmp[n++], off / 2.0, off / 2.0, -off / 2.0, z + off * 1.5, 0, 0, 0, 1.0, 1.0, 1.0, 1);
+            put(&tmp[n++], off / 2.0, -off / 2.0, -off / 2.0, z + off * 1.5, 0, 0, 0, 1.0, 1.0, 1.0, 2);
+            cfg->vertical_fov_radians = 0.5;
+        } else {
+            put(&tmp[n++], off / 2.0, 0.0, 0.0 + off / 4.0, z + off * 1.5, 1.92, 1.91, 1.9, 1.92, 1.91, 1.9, 0);
+            put(&tmp[n++], off / 2.0, off / 2.0, -off / 2.0, z + off, 0, 0, 0, 1.0, 1.0, 1.0, 1);
+            put(&tmp[n++], off / 2.0, -off / 2.0, -off / 2.0, z + off, 0, 0, 0, 1.0, 1.0, 1.0, 2);
+            cfg->vertical_fov_radians = 0.75;
+        }
+        cfg->position[2] = 2.0;
+        cfg->direction[2] = z + off * 1.5;
+    } else {
+        return -1;
+    }
+    cfg->aspect_ratio = (w * 1.0) / (h * 1.0);
+    cfg->aperture = 0.2;
+    double diff[3] = {cfg->position[0] - cfg->direction[0], cfg->position[1] - cfg->direction[1],
+                      cfg->position[2] - cfg->direction[2]};
+    cfg->focus_distance = po_vec_length(diff);
+    if (n > cap)
+        return -1;
+    memcpy(out, tmp, sizeof(po_sphere) * (size_t)n);
+    return n;
+}
+
+/* Synthetic scene (BASELINE.json configs[4]; the reference has none, the
+ * generator is defined in DESIGN.md "Synthetic scene"). */
+int po_scene_synthetic(int n, int w, int h, uint32_t gen_seed, po_sphere *out, po_camera_config *cfg)
+{
+    if (n < 2)
+        return -1;
+    po_mt19937 g;
+    po_mt_seed(&g, gen_seed);
+    cfg_defaults(cfg);
+    put(&out[0], 1000.0, 0.0, -1000.0, 0.0, 0, 0, 0, 0.5, 0.5, 0.5, 0);
+    put(&out[1], 2.0, 0.0, 8.0, 0.0, 8.0, 8.0, 8.0, 0.8, 0.8, 0.8, 0);
+    for (int i = 2; i < n; ++i) {
+        double r = 0.05 + 0.1 * po_mt_generate(&g);
+        double x = -10.0 + 20.0 * po_mt_generate(&g);
+        double z = -10.0 + 20.0 * po_mt_generate(&g);
+        double m = po_mt_generate(&g);
+        double cr = 0.2 + 0.75 * po_mt_generate(&g);
+        double cg = 0.2 + 0.75 * po_mt_generate(&g);
+        double cbl = 0.2 + 0.75 * po_mt_generate(&g);
+        int mat = m < 0.80 ? 0 : (m < 0.95 ? 1 : 2);
+        put(&out[i], r, x, r, z, 0, 0, 0, cr, cg, cbl, mat);
+    }
+    cfg->position[0] = 0.0; cfg->position[1] = 2.0; cfg->position[2] = 12.0;
+    cfg->vertical_fov_radians = 0.8;
+    cfg->aspect_ratio = (w * 1.0) / (h * 1.0);
+    cfg->aperture = 0.0;
+    double diff[3] = {cfg->position[0] - cfg->direction[0], cfg->position[1] - cfg->direction[1],
+                      cfg->position[2] - cfg->direction[2]};
+    cfg->focus_distance = po_vec_length(diff);
+    return n;
+}

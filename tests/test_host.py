@@ -1,0 +1,115 @@
+"""CPU tests of the host side: the C ABI library loads and exports every
+declared symbol, the host mirrors of the reference's scenes/camera are
+bit-exact against the compiled reference's dumps, shard geometry, and the
+error behaviour of the ABI (no GPU compute is launched here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import ptgpu
+import pyoracle as po
+from conftest import ROOT
+
+SIZES = {"box": ["1024x768", "1920x1080", "3840x2160"], "box_mirror": ["1024x768", "1920x1080", "3840x2160"],
+         "simple": ["400x300"]}
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "ptgpu.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ptg_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    syms = _header_symbols()
+    assert len(syms) == len(ptgpu.EXPORTS) and set(syms) == set(ptgpu.EXPORTS)
+    lib = C.CDLL(ptgpu.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", ptgpu.LIB_PATH], capture_output=True, text=True).stdout
+    for s in syms:
+        assert re.search(rf"\bT {s}\b", out), s
+    assert ptgpu.lib().ptg_abi_version() == ptgpu.ABI_VERSION
+
+
+def test_library_is_gfx950_code():
+    with open(ptgpu.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+@pytest.mark.parametrize("name", ["box", "box_mirror", "simple"])
+def test_host_scenes_bitexact_vs_reference(golden, name):
+    for tag in SIZES[name]:
+        ref = golden[name]["scene_" + tag]
+        scn = ptgpu.make_scene(name, ref["w"], ref["h"])
+        arr = scn.to_array()
+        assert len(arr) == len(ref["spheres"])
+        for s, r in zip(arr, ref["spheres"]):
+            assert float(s["radius"]) == r["radius"]
+            assert list(s["position"]) == r["position"]
+            assert list(s["emission"]) == r["emission"]
+            assert list(s["color"]) == r["color"]
+            assert int(s["material"]) == r["material"]
+        c = scn.camera_parameters
+        for k, v in ref["camera_config"].items():
+            got = getattr(c, k)
+            assert (list(got) if isinstance(got, tuple) else got) == v, k
+        cam = ptgpu.camera.with_config(c)
+        for k, v in ref["camera"].items():
+            got = getattr(cam, k)
+            assert (list(got) if isinstance(got, tuple) else got) == v, k
+
+
+def test_synthetic_scene_matches_oracle_generator():
+    scn = ptgpu.synthetic_scene(500, 1920, 1080, 42)
+    ref, cfg = po.synthetic_scene(500, 1920, 1080, 42)
+    assert scn.to_array().tobytes() == ref.tobytes()
+    c = scn.camera_parameters
+    assert list(c.position) == list(cfg[0]["position"]) and c.focus_distance == cfg[0]["focus_distance"]
+
+
+@pytest.mark.parametrize("H,br,count", [(1080, 8, 1), (1080, 8, 3), (1080, 8, 8), (768, 16, 4), (23, 8, 2),
+                                        (7, 4, 5)])
+def test_shard_rows_cover_image_exactly_once(H, br, count):
+    seen = np.concatenate([ptgpu.slab_to_image_rows(H, br, k, count) for k in range(count)])
+    seen = seen[seen >= 0]
+    assert sorted(seen.tolist()) == list(range(H))
+    W = 5
+    rows = ptgpu.shard_rows(H, br, count)
+    full = np.random.default_rng(0).random((H, W, 3)).astype(np.float32)
+    gathered = np.zeros((count, rows, W, 3), np.float32)
+    for k in range(count):
+        m = ptgpu.slab_to_image_rows(H, br, k, count)
+        gathered[k][m >= 0] = full[m[m >= 0]]
+    assert np.array_equal(ptgpu.unshard_host(gathered, W, H, br, count), full)
+
+
+def test_abi_rejects_bad_arguments_without_gpu_work():
+    L = ptgpu.lib()
+    out = C.c_int32()
+    assert L.ptg_shard_rows(0, 8, 1, C.byref(out)) == -1
+    assert L.ptg_shard_rows(1080, 8, 8, C.byref(out)) == 0 and out.value == 136
+    scn = ptgpu.box_scene(8, 8)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    img = np.zeros((64, 3))
+    with pytest.raises(ptgpu.PtgError, match="num_subpixels"):
+        ptgpu.render(scn, cam, img, 8, 8, 4, num_subpixels=0)
+    with pytest.raises(ptgpu.PtgError, match="samples"):
+        ptgpu.render(scn, cam, img, 8, 8, -3)
+    with pytest.raises(ValueError):
+        ptgpu.render(scn, cam, np.zeros((10, 3)), 8, 8, 4)
+    bad = scn.to_array()
+    bad[0]["material"] = 7
+    with pytest.raises(ptgpu.PtgError, match="invalid"):
+        ptgpu.Context(bad, cam)
+
+
+def test_params_struct_matches_header():
+    assert C.sizeof(ptgpu.Params) == 48
+    p = ptgpu.make_params(1920, 1080, 256)
+    assert (p.width, p.height, p.samples, p.num_subpixels, p.band_rows, p.shard_count) == (1920, 1080, 256, 2, 8, 1)
