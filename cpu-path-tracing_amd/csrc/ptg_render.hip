@@ -64,7 +64,7 @@ struct KArgs {
     // image / sampling
     int W, H, samps, nsub, lanes_per_pixel, pixels_per_wave, waves_per_row;
     int slab_rows, band_rows, shard_rank, shard_count;
-    float fW, fH, inv_samps, sub_len, inv_sub2;
+    float invW, invH, inv_samps, sub_len, inv_sub2;
     unsigned long long seed;
     int chunk, n_groups, single_chunk;
     long long n_units;
@@ -87,8 +87,8 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
     float u2 = draw(st);
     float xin = __builtin_fmaf(A.sub_len, u1, (float)L.x + (float)L.sx * A.sub_len);
     float yin = __builtin_fmaf(A.sub_len, u2, (float)L.y + (float)L.sy * A.sub_len);
-    float fs = xin / A.fW;
-    float ft = yin / A.fH;
+    float fs = xin * A.invW;  // main.cpp:190 x/W as x * (1/W)
+    float ft = yin * A.invH;
     // camera.cpp:19-30: rejection sample of the unit disk (2 draws per try)
     float px, py;
     do {
@@ -107,9 +107,16 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 
 // main.cpp:30-42 + sphere.cpp:6-30: closest root >= eps over all spheres,
 // strict < so the lowest index wins ties.  Sphere records are loaded with
-// wave-uniform addresses -> scalar loads.
-template <bool kLds>
-__device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
+// wave-uniform addresses -> scalar loads (SGPR operands, no VGPR/LDS traffic).
+// Roots: with q = -(hb + sign(hb) sqrt(disc)) they are c/q and q/a; c/q is
+// the nearer one whenever hb < 0, so one division per candidate and the far
+// root q/a only when the near one is < eps.  Two exact culls skip spheres that
+// cannot win without the sqrt/division (DESIGN.md "scene scan"):
+//   hb >= 0 && c >= 0                      both roots <= 0
+//   hb < 0 && c > 0 && c >= tb*2|hb|*(1+2^-20)  near root c/q > tb (q <= 2|hb|(1+3u))
+constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20
+
+__device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *__restrict__ geo, f3 o, f3 d, float &tbest)
 {
     float a = dot3(d, d);
     float tb = kInf;
@@ -128,22 +135,30 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             hb = ed;
             c = ee + g1.w;
         }
+        if (hb >= 0.0f && c >= 0.0f)
+            continue;
+        if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * kCullMargin)
+            continue;
         float disc = __builtin_fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
-        float sq = __builtin_sqrtf(disc);
-        float q = -(hb + __builtin_copysignf(sq, hb));
-        float t1 = q / a;
-        float t2 = c / q;
-        float tmin = t1 < t2 ? t1 : t2;
-        float tmax = t1 < t2 ? t2 : t1;
-        float root = tmin;
-        if (root < kEps) {
-            root = tmax;
-            if (root < kEps)
+        float sq = sqrt_d(disc);
+        float root;
+        if (hb < 0.0f) {
+            float q = sq - hb;
+            root = c / q;
+            if (root < kEps) {
+                root = q / a;
+                if (root < kEps)
+                    continue;
+            }
+        } else {
+            float q = -(hb + sq);
+            root = c / q;
+            if (!(root >= kEps))
                 continue;
         }
-        if (root > 0.0f && root < tb) {
+        if (root < tb) {
             tb = root;
             id = i;
         }
@@ -155,12 +170,10 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
-template <bool kLds>
-__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o, f3 &d, f3 &T, f3 &E, int &depth,
-                                        uint32_t &st)
+__device__ __forceinline__ bool segment(const KArgs &A, f3 &o, f3 &d, f3 &T, f3 &E, int &depth, uint32_t &st)
 {
     float t;
-    int id = scene_scan<kLds>(A, geo, o, d, t);
+    int id = scene_scan(A, A.geo, o, d, t);
     if (id < 0) {  // main.cpp:115-120: sky
         f3 ud = norm3(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -174,7 +187,9 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o
     float4 s0 = S.s0, s1 = S.s1;
     // hit_record.cpp:3-12
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
-    f3 on = norm3(mk3(p.x - s0.x, p.y - s0.y, p.z - s0.z));
+    // hit_record.cpp:6 (p - C).norm() as (p - C) * (1/R): p lies on the sphere
+    const float invR = S.s2.w;
+    f3 on = mk3((p.x - s0.x) * invR, (p.y - s0.y) * invR, (p.z - s0.z) * invR);
     bool front = dot3(on, d) < 0.0f;
     f3 nn = front ? on : mk3(-on.x, -on.y, -on.z);
     // main.cpp:126
@@ -197,8 +212,8 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o
         float ra = draw(st);
         float cp, sp;
         sincos2pi(u_phi, cp, sp);
-        float sth = __builtin_sqrtf(ra);
-        float cth = __builtin_sqrtf(1.0f - ra);
+        float sth = sqrt_d(ra);
+        float cth = sqrt_d(1.0f - ra);
         f3 w = nn;
         f3 uu = __builtin_fabsf(w.x) > 0.1f ? mk3(w.z, 0.0f, -w.x) : mk3(0.0f, -w.z, w.y);
         uu = norm3(uu);
@@ -208,17 +223,16 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o
                     __builtin_fmaf(w.y, cth, __builtin_fmaf(vv.y, ss, uu.y * cs)),
                     __builtin_fmaf(w.z, cth, __builtin_fmaf(vv.z, ss, uu.z * cs)));
         o = p;
-        d = norm3(nd);
+        d = nd;  // unit by construction (main.cpp:55 re-normalises it)
     } else if (mat == PTG_DIELECTRIC) {  // main.cpp:69-97
         float ratio = front ? 0.5f : 2.0f;
         f3 ud = norm3(d);
         float x0 = -dot3(ud, nn);
         float cth = 1.0f < x0 ? 1.0f : x0;
-        float sth = __builtin_sqrtf(__builtin_fmaf(-cth, cth, 1.0f));
+        float sth = sqrt_d(__builtin_fmaf(-cth, cth, 1.0f));
         bool reflect = ratio * sth > 1.0f;  // cannot refract: no Fresnel draw
         if (!reflect) {
-            float r0 = (1.0f - ratio) / (1.0f + ratio);
-            r0 = r0 * r0;
+            const float r0 = 0x1.c71c74p-4f;  // ((1-ratio)/(1+ratio))^2, equal for ratio 0.5 and 2
             float xm = 1.0f - cth;
             float x2 = xm * xm;
             float x5 = (x2 * x2) * xm;
@@ -230,7 +244,7 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o
         } else {
             f3 perp = mk3(__builtin_fmaf(nn.x, cth, ud.x) * ratio, __builtin_fmaf(nn.y, cth, ud.y) * ratio,
                           __builtin_fmaf(nn.z, cth, ud.z) * ratio);
-            float sq = __builtin_sqrtf(__builtin_fabsf(1.0f - dot3(perp, perp)));
+            float sq = sqrt_d(__builtin_fabsf(1.0f - dot3(perp, perp)));
             o = p;
             d = mk3(__builtin_fmaf(nn.x, -sq, perp.x), __builtin_fmaf(nn.y, -sq, perp.y),
                     __builtin_fmaf(nn.z, -sq, perp.z));
@@ -255,13 +269,19 @@ __device__ __forceinline__ int out_row_of(const KArgs &A, int slab_row)
 }
 
 // Exact per-path quantisation (include/ptgpu.h "Sample accumulation").
+// trunc(c * 2^32) for c in [0, 2^30] without double arithmetic: integer part
+// and fraction * 2^32 are both exact in fp32, so this equals the oracle's
+// (uint64_t)((double)c * 0x1p32) bit for bit.
 __device__ __forceinline__ unsigned long long quant(float c)
 {
     if (!(c >= 0.0f))
         return 0ull;
     if (c > 0x1p30f)
         c = 0x1p30f;
-    return (unsigned long long)((double)c * 0x1p32);
+    float ip = __builtin_truncf(c);
+    uint32_t hi = (uint32_t)ip;
+    uint32_t lo = (uint32_t)((c - ip) * 0x1p32f);
+    return ((unsigned long long)hi << 32) | lo;
 }
 
 // One work unit per wave: a pixel group (pixels_per_wave pixels of one slab
@@ -315,8 +335,14 @@ __global__ __launch_bounds__(kBlock) void render_kernel(KArgs A)
     uint32_t st = 0;
     uint32_t segs = 0;
     auto start = [&](int it) {
-        slot = it % nv;
-        int sample = s0 + it / nv;
+        int sample;
+        if (nv == 64) {  // full pixel group (the common case): shifts
+            slot = it & 63;
+            sample = s0 + (it >> 6);
+        } else {
+            slot = it % nv;
+            sample = s0 + it / nv;
+        }
         Lane L;
         int ps = slot / A.lanes_per_pixel;
         int sub = slot - ps * A.lanes_per_pixel;
@@ -339,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(KArgs A)
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            done = segment<false>(A, A.geo, o, d, T, E, depth, st);
+            done = segment(A, o, d, T, E, depth, st);
             if (done) {
                 atomicAdd(&lds_acc[wv][slot], quant(E.x));
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
@@ -432,7 +458,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     bool done = false;
     while (!done) {
         segs += 1;
-        done = segment<false>(A, A.geo, o, d, T, E, depth, st);
+        done = segment(A, o, d, T, E, depth, st);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -536,7 +562,7 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
         std::memcpy(&matf, &mat, 4);
         r.s0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], p);
         r.s1 = make_float4((float)sp.emission[0], (float)sp.emission[1], (float)sp.emission[2], matf);
-        r.s2 = make_float4(cx, cy, cz, 0.0f);
+        r.s2 = make_float4(cx, cy, cz, (float)(1.0 / R));
         r.s3 = make_float4(rx, ry, rz, 0.0f);
         shade[i] = r;
     }
@@ -574,14 +600,22 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     A.band_rows = p->band_rows;
     A.shard_rank = p->shard_rank;
     A.shard_count = p->shard_count;
-    A.fW = (float)p->width;
-    A.fH = (float)p->height;
+    A.invW = 1.0f / (float)p->width;
+    A.invH = 1.0f / (float)p->height;
     A.inv_samps = p->samples > 0 ? 1.0f / (float)p->samples : 0.0f;
     A.sub_len = 1.0f / (float)p->num_subpixels;
     A.inv_sub2 = 1.0f / (float)(p->num_subpixels * p->num_subpixels);
     A.seed = p->seed;
     // work unit = pixel group x chunk of samples (auto: 32 samples per sub-pixel)
-    int chunk = p->chunk_samples > 0 ? p->chunk_samples : 32;
+    // auto: split the samples only as far as needed for ~96k work units (about
+    // 16 waves per SIMD slot on 256 CUs), which keeps the grid-level tail small
+    const int groups = A.slab_rows * A.waves_per_row;
+    int chunk = p->chunk_samples;
+    if (chunk <= 0) {
+        long long want = (98304 + groups - 1) / groups;
+        long long nch = want < 1 ? 1 : (want > p->samples ? p->samples : want);
+        chunk = nch > 0 ? (int)((p->samples + nch - 1) / nch) : 1;
+    }
     if (chunk > p->samples)
         chunk = p->samples > 0 ? p->samples : 1;
     A.chunk = chunk;

@@ -524,9 +524,29 @@ int po_render_xs_f64(const po_sphere *s, int n, const po_camera *cam, int W, int
 typedef struct { float x, y, z; } f3;
 static f3 fk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
 static float fdot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+/* Deterministic reciprocal square root (DESIGN.md "fp32 math"): bit-trick seed
+ * + two Newton steps written with explicit fmaf, so CPU and GPU agree bit for
+ * bit; about 2 ulp, x > 0. */
+static float rsqrt_B(float x)
+{
+    uint32_t i;
+    memcpy(&i, &x, 4);
+    i = 0x5f375a86u - (i >> 1);
+    float y;
+    memcpy(&y, &i, 4);
+    float h = 0.5f * x;
+    float t = y * y;
+    t = fmaf(-h, t, 1.5f);
+    y = y * t;
+    t = y * y;
+    t = fmaf(-h, t, 1.5f);
+    return y * t;
+}
+/* sqrt(x) = x * rsqrt(x); 0 for x <= 0 */
+static float sqrt_B(float x) { return x > 0.0f ? x * rsqrt_B(x) : 0.0f; }
 static f3 fnorm(f3 a)
 {
-    float inv = 1.0f / sqrtf(fdot(a, a));
+    float inv = rsqrt_B(fdot(a, a));
     return fk(a.x * inv, a.y * inv, a.z * inv);
 }
 static f3 fcross(f3 a, f3 b)
@@ -536,7 +556,7 @@ static f3 fcross(f3 a, f3 b)
 
 typedef struct {
     f3 P, N;          /* anchor point and anchor normal (big) or centre and 0 */
-    float R, R2x, negR2;
+    float R, R2x, negR2, invR;
     int big;
     f3 C;             /* centre (float) for normals */
     f3 emis, col, col_rr;
@@ -546,7 +566,7 @@ typedef struct {
 
 typedef struct {
     f3 pos, base, X, Y; /* base = float(llc - pos) */
-    float lens;
+    float lens, invW, invH;
 } camB;
 
 static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
@@ -559,6 +579,7 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         b->R = (float)R;
         b->R2x = (float)(2.0 * R);
         b->negR2 = (float)(-(R * R));
+        b->invR = (float)(1.0 / R);
         if (b->big) {
             double vx = cam->position[0] - sp->position[0];
             double vy = cam->position[1] - sp->position[1];
@@ -599,6 +620,8 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
     cb->X = fk((float)cam->cam_x_axis[0], (float)cam->cam_x_axis[1], (float)cam->cam_x_axis[2]);
     cb->Y = fk((float)cam->cam_y_axis[0], (float)cam->cam_y_axis[1], (float)cam->cam_y_axis[2]);
     cb->lens = (float)cam->lens_radius;
+    cb->invW = 0.0f;
+    cb->invH = 0.0f;
 }
 
 /* sin/cos of 2*pi*u for u in [0,1): quadrant split of 4u (exact) and Taylor
@@ -632,7 +655,12 @@ static void sincos2pi_B(float u, float *c, float *s)
 }
 
 /* Scene scan, Mode B (main.cpp:30-42 + sphere.cpp:6-30 with the stable
- * quadratic roots; huge spheres use the anchored form) */
+ * quadratic roots; huge spheres use the anchored form).  With
+ * q = -(hb + sign(hb) sqrt(disc)) the roots are c/q and q/a, and c/q is the
+ * nearer one whenever hb < 0; the nearest root >= eps is therefore c/q, else
+ * (hb < 0 only) q/a.  Two exact culls skip spheres that provably cannot win
+ * (they never change the result: DESIGN.md "scene scan"). */
+#define CULL_MARGIN 0x1.00001p+0f /* 1 + 2^-20 */
 static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
 {
     float a = fdot(d, d);
@@ -651,21 +679,30 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
             hb = ed;
             c = ee + sp->negR2;
         }
+        if (hb >= 0.0f && c >= 0.0f)
+            continue; /* both roots <= 0 */
+        if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * CULL_MARGIN)
+            continue; /* near root provably > tb */
         float disc = fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
-        float sq = sqrtf(disc);
-        float q = -(hb + copysignf(sq, hb));
-        float t1 = q / a, t2 = c / q;
-        float tmin = t1 < t2 ? t1 : t2;
-        float tmax = t1 < t2 ? t2 : t1;
-        float root = tmin;
-        if (root < EPSF) {
-            root = tmax;
-            if (root < EPSF)
+        float sq = sqrt_B(disc);
+        float root;
+        if (hb < 0.0f) {
+            float q = sq - hb;
+            root = c / q;
+            if (root < EPSF) {
+                root = q / a;
+                if (root < EPSF)
+                    continue;
+            }
+        } else {
+            float q = -(hb + sq);
+            root = c / q;
+            if (!(root >= EPSF))
                 continue;
         }
-        if (root > 0.0f && root < tb) {
+        if (root < tb) {
             tb = root;
             id = i;
         }
@@ -675,7 +712,7 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
     return tb < INFF;
 }
 
-static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub, int x, int y, int sx, int sy,
+static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y, int sx, int sy,
                    uint32_t st, int *segs)
 {
     float sl = 1.0f / (float)nsub;
@@ -683,7 +720,7 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub
     float u2 = po_xs_f32(&st);
     float xin = fmaf(sl, u1, (float)x + (float)sx * sl);
     float yin = fmaf(sl, u2, (float)y + (float)sy * sl);
-    float fs = xin / (float)W, ft = yin / (float)H;
+    float fs = xin * cam->invW, ft = yin * cam->invH; /* main.cpp:190 x/W, y/H as x * (1/W) */
     float px, py;
     for (;;) {
         px = fmaf(2.0f, po_xs_f32(&st), -1.0f);
@@ -714,7 +751,8 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub
         }
         const sphB *sp = &s[id];
         f3 p = fk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z));
-        f3 on = fnorm(fk(p.x - sp->C.x, p.y - sp->C.y, p.z - sp->C.z));
+        /* hit_record.cpp:6: (p - C).norm(), as (p - C) * (1/R): p lies on the sphere */
+        f3 on = fk((p.x - sp->C.x) * sp->invR, (p.y - sp->C.y) * sp->invR, (p.z - sp->C.z) * sp->invR);
         int front = fdot(on, d) < 0.0f;
         f3 nn = front ? on : fk(-on.x, -on.y, -on.z);
         E = fk(fmaf(T.x, sp->emis.x, E.x), fmaf(T.y, sp->emis.y, E.y), fmaf(T.z, sp->emis.z, E.z));
@@ -732,8 +770,8 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub
             float ra = po_xs_f32(&st);
             float cp, sp_;
             sincos2pi_B(u_phi, &cp, &sp_);
-            float sth = sqrtf(ra);
-            float cth = sqrtf(1.0f - ra);
+            float sth = sqrt_B(ra);
+            float cth = sqrt_B(1.0f - ra);
             f3 w = nn;
             f3 uu = fabsf(w.x) > 0.1f ? fk(w.z, 0.0f, -w.x) : fk(0.0f, -w.z, w.y);
             uu = fnorm(uu);
@@ -741,21 +779,20 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub
             float cs = cp * sth, ss = sp_ * sth;
             f3 nd = fk(fmaf(w.x, cth, fmaf(vv.x, ss, uu.x * cs)), fmaf(w.y, cth, fmaf(vv.y, ss, uu.y * cs)),
                        fmaf(w.z, cth, fmaf(vv.z, ss, uu.z * cs)));
-            o = p;
-            d = fnorm(nd);
+            o = p; /* main.cpp:55 normalises u*cos*sin + v*sin*sin + w*cos, a unit vector by construction */
+            d = nd;
             continue;
         } else if (sp->mat == 2) { /* dielectric, main.cpp:69-97 */
             float ratio = front ? 0.5f : 2.0f;
             f3 ud = fnorm(d);
             float x0 = -fdot(ud, nn);
             float cth = 1.0f < x0 ? 1.0f : x0;
-            float sth = sqrtf(fmaf(-cth, cth, 1.0f));
+            float sth = sqrt_B(fmaf(-cth, cth, 1.0f));
             int cannot = ratio * sth > 1.0f;
             if (cannot) {
                 reflect = 1;
             } else {
-                float r0 = (1.0f - ratio) / (1.0f + ratio);
-                r0 = r0 * r0;
+                const float r0 = 0x1.c71c74p-4f; /* ((1-ratio)/(1+ratio))^2 for ratio 0.5 and 2 */
                 float xm = 1.0f - cth;
                 float x2 = xm * xm;
                 float x5 = (x2 * x2) * xm;
@@ -765,7 +802,7 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int W, int H, int nsub
             if (!reflect) {
                 f3 perp = fk(fmaf(nn.x, cth, ud.x) * ratio, fmaf(nn.y, cth, ud.y) * ratio,
                              fmaf(nn.z, cth, ud.z) * ratio);
-                float sq = sqrtf(fabsf(1.0f - fdot(perp, perp)));
+                float sq = sqrt_B(fabsf(1.0f - fdot(perp, perp)));
                 o = p;
                 d = fk(fmaf(nn.x, -sq, perp.x), fmaf(nn.y, -sq, perp.y), fmaf(nn.z, -sq, perp.z));
                 continue;
@@ -800,13 +837,13 @@ static float mean_B(uint64_t sum, int samps)
     return samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)samps) : 0.0f;
 }
 
-static f3 subpixel_B(const sphB *s, int n, const camB *cam, int W, int H, int samps, int nsub, int x, int y,
+static f3 subpixel_B(const sphB *s, int n, const camB *cam, int samps, int nsub, int x, int y,
                      int sx, int sy, uint64_t key, uint64_t *segs)
 {
     uint64_t ax = 0, ay = 0, az = 0;
     for (int k = 0; k < samps; ++k) {
         int sg = 0;
-        f3 c = sample_B(s, n, cam, W, H, nsub, x, y, sx, sy, po_sample_state(key, (uint32_t)k), &sg);
+        f3 c = sample_B(s, n, cam, nsub, x, y, sx, sy, po_sample_state(key, (uint32_t)k), &sg);
         *segs += (uint64_t)sg;
         ax += quant_B(c.x);
         ay += quant_B(c.y);
@@ -825,6 +862,8 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
     sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
     camB cb;
     prep_B(s, n, cam, sb, &cb);
+    cb.invW = 1.0f / (float)W;
+    cb.invH = 1.0f / (float)H;
     uint64_t total = 0;
     float q = 1.0f / (float)(nsub * nsub);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
@@ -836,7 +875,7 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
                     uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) +
                                   (uint64_t)(sy * nsub + sx);
                     uint64_t segs = 0;
-                    f3 a = subpixel_B(sb, n, &cb, W, H, samps, nsub, x, y, sx, sy, po_key_hash(seed, ps), &segs);
+                    f3 a = subpixel_B(sb, n, &cb, samps, nsub, x, y, sx, sy, po_key_hash(seed, ps), &segs);
                     total += segs;
                     pix = fk(fmaf(clampf_B(a.x), q, pix.x), fmaf(clampf_B(a.y), q, pix.y),
                              fmaf(clampf_B(a.z), q, pix.z));
@@ -859,9 +898,11 @@ int po_sample_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H,
     sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
     camB cb;
     prep_B(s, n, cam, sb, &cb);
+    cb.invW = 1.0f / (float)W;
+    cb.invH = 1.0f / (float)H;
     uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) + (uint64_t)(sy * nsub + sx);
     int segs = 0;
-    f3 c = sample_B(sb, n, &cb, W, H, nsub, x, y, sx, sy, po_sample_state(po_key_hash(seed, ps), sample), &segs);
+    f3 c = sample_B(sb, n, &cb, nsub, x, y, sx, sy, po_sample_state(po_key_hash(seed, ps), sample), &segs);
     out[0] = c.x;
     out[1] = c.y;
     out[2] = c.z;
