@@ -48,6 +48,9 @@ int fail(int code, const std::string &msg)
     } while (0)
 
 constexpr int kBlock = 256;        // 4 waves per workgroup
+#ifndef PTG_MIN_WAVES_PER_EU
+#define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
+#endif
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr double kBigRadius = 1000.0;
 
@@ -146,7 +149,11 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *__restri
         float root;
         if (hb < 0.0f) {
             float q = sq - hb;
+#ifdef PTG_RCP  // speed probe only
+            root = c * (1.0f / q);
+#else
             root = c / q;
+#endif
             if (root < kEps) {
                 root = q / a;
                 if (root < kEps)
@@ -292,12 +299,15 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
 template <bool kCount>
-__global__ __launch_bounds__(kBlock) void render_kernel(KArgs A)
+__global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
     __shared__ unsigned long long lds_acc[kWavesPerBlock][64 * 3];
     __shared__ unsigned long long lds_key[kWavesPerBlock][64];
+    __shared__ uint32_t lds_pix[kWavesPerBlock][64];  // slot -> x | sx << 20 | sy << 26
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+    // wave-uniform by construction; readfirstlane lets the compiler keep all
+    // per-unit bookkeeping in SGPRs
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const long long unit = (long long)blockIdx.x * kWavesPerBlock + wv;
     if (unit >= A.n_units)
         return;  // whole wave
@@ -322,8 +332,11 @@ __global__ __launch_bounds__(kBlock) void render_kernel(KArgs A)
     if (lane < nv) {
         int px = x0 + lane / A.lanes_per_pixel;
         int sub = lane % A.lanes_per_pixel;
+        int sy = sub / A.nsub;
+        int sx = sub - sy * A.nsub;
         uint64_t ps = ((uint64_t)y * (uint64_t)A.W + (uint64_t)px) * (uint64_t)A.lanes_per_pixel + (uint64_t)sub;
         lds_key[wv][lane] = key_hash(A.seed, ps);
+        lds_pix[wv][lane] = (uint32_t)px | ((uint32_t)sx << 20) | ((uint32_t)sy << 26);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -344,12 +357,11 @@ __global__ __launch_bounds__(kBlock) void render_kernel(KArgs A)
             sample = s0 + it / nv;
         }
         Lane L;
-        int ps = slot / A.lanes_per_pixel;
-        int sub = slot - ps * A.lanes_per_pixel;
-        L.x = x0 + ps;
+        uint32_t pk = lds_pix[wv][slot];
+        L.x = (int)(pk & 0xFFFFFu);
         L.y = y;
-        L.sy = sub / A.nsub;
-        L.sx = sub - L.sy * A.nsub;
+        L.sx = (int)((pk >> 20) & 63u);
+        L.sy = (int)(pk >> 26);
         L.key = lds_key[wv][slot];
         camera_ray(A, L, (uint32_t)sample, st, o, d);
         T = mk3(1.0f, 1.0f, 1.0f);
@@ -580,7 +592,7 @@ int check_params(const ptg_params *p)
         return fail(PTG_ERR_UNSUPPORTED, "num_subpixels must be in [1, 8]");
     if (p->band_rows < 1 || p->shard_count < 1 || p->shard_rank < 0 || p->shard_rank >= p->shard_count)
         return fail(PTG_ERR_INVALID_ARGUMENT, "invalid shard (band_rows >= 1, 0 <= rank < count)");
-    if ((int64_t)p->width * p->height > (int64_t)1 << 28)
+    if ((int64_t)p->width * p->height > (int64_t)1 << 28 || p->width >= (1 << 20))
         return fail(PTG_ERR_UNSUPPORTED, "image too large");
     return PTG_OK;
 }

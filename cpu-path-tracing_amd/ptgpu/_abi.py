@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libptgpu.so")
+# PTGPU_LIB selects an alternative build of the same ABI (A/B experiments only)
+LIB_PATH = os.environ.get("PTGPU_LIB") or os.path.join(PKG_DIR, "libptgpu.so")
 ABI_VERSION = 1
 
 # every symbol include/ptgpu.h declares
