@@ -114,10 +114,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    # PTG_REHEARSAL=1: N ranks on one GPU with gloo (single-GPU box rehearsal
+    # of the sharded path); the real multi-GPU run uses nccl (RCCL over xGMI)
+    rehearsal = os.environ.get("PTG_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     nsub = 2  # main.cpp:202
     W, H = args.width, args.height
@@ -167,10 +175,11 @@ def main():
 
     seg_total = seg_local
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        cdev = torch.device("cpu") if rehearsal else dev
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-        s = torch.tensor([seg_local], dtype=torch.int64, device=dev)
+        elapsed = float(t[0])
+        s = torch.tensor([seg_local], dtype=torch.int64, device=cdev)
         dist.all_reduce(s)
         seg_total = int(s.item())
     frame_samples = W * H * spp
@@ -203,7 +212,9 @@ def main():
             "config": {"workload": workload, "scene": args.scene, "width": W, "height": H, "spp": spp,
                        "samples_per_subpixel": samps, "num_subpixels": nsub, "spheres": n_sph,
                        "band_rows": args.band_rows, "chunk_samples": args.chunk or "auto",
-                       "parallelism": f"tile-sharded row bands x{world}" if world > 1 else "single GPU"},
+                       "parallelism": (f"tile-sharded row bands x{world}" + (" (gloo rehearsal on one GPU)"
+                                                                              if rehearsal else ""))
+                       if world > 1 else "single GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3) if achieved else None,
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,

@@ -192,9 +192,15 @@ def render_sharded(params: Params, slab, group=None,
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     assert params.shard_count == world and params.shard_rank == rank
+    # gloo cannot gather device tensors: stage through host memory (CPU
+    # rehearsals only; the nccl backend (RCCL) gathers HBM to HBM over xGMI)
+    staged = slab.is_cuda and dist.get_backend(group) == "gloo"
+    send = slab.cpu() if staged else slab
     if rank == 0:
-        gathered = torch.empty((world,) + tuple(slab.shape), dtype=slab.dtype, device=slab.device)
-        dist.gather(slab, gather_list=list(gathered.unbind(0)), dst=0, group=group)
+        gathered = torch.empty((world,) + tuple(send.shape), dtype=send.dtype, device=send.device)
+        dist.gather(send, gather_list=list(gathered.unbind(0)), dst=0, group=group)
+        if staged:
+            gathered = gathered.to(slab.device)
         image = torch.empty((params.height, params.width, 3), dtype=slab.dtype, device=slab.device)
         if unshard is not None:
             unshard(gathered, image, params)
@@ -204,5 +210,5 @@ def render_sharded(params: Params, slab, group=None,
             image.copy_(torch.from_numpy(unshard_host(gathered.numpy(), params.width, params.height,
                                                        params.band_rows, world)))
         return image
-    dist.gather(slab, gather_list=None, dst=0, group=group)
+    dist.gather(send, gather_list=None, dst=0, group=group)
     return None

@@ -17,5 +17,6 @@ BENCH=(bench.py --steps 2 --warmup 1 --cpu-baseline off "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_trace.json" 2> "$out/trace.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_fetch.json" 2> "$out/fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_write.json" 2> "$out/write.err"
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES -d "$out/sq" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_sq.json" 2> "$out/sq.err"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY -d "$out/sq" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_sq.json" 2> "$out/sq.err"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SMEM -d "$out/sq2" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_sq2.json" 2> "$out/sq2.err"
 echo "profile $tag done"

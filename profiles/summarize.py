@@ -36,6 +36,9 @@ def main(src, tag, kernel_sub="render_kernel"):
     fetch, _ = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), kernel_sub)
     write, _ = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), kernel_sub)
     sq, rows = per_kernel(os.path.join(src, "sq", "run_counter_collection.csv"), kernel_sub)
+    sq2p = os.path.join(src, "sq2", "run_counter_collection.csv")
+    if os.path.exists(sq2p):
+        sq.update(per_kernel(sq2p, kernel_sub)[0])
     fetch_b = fetch.get("FETCH_SIZE", 0.0) * 1024 * 2  # gfx950 FETCH_SIZE = 1/2 of wide-stream bytes
     write_b = write.get("WRITE_SIZE", 0.0) * 1024
     out["hbm_bytes_per_launch"] = {"fetch_x2": fetch_b, "write": write_b, "total": fetch_b + write_b}
