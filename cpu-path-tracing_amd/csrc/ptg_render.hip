@@ -48,6 +48,9 @@ int fail(int code, const std::string &msg)
     } while (0)
 
 constexpr int kBlock = 256;        // 4 waves per workgroup
+#ifndef PTG_RESTART_BATCH
+#define PTG_RESTART_BATCH 8  // measured: 8 beats 1, 4, 16 (profiles/)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -112,17 +115,21 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 // strict < so the lowest index wins ties.  Sphere records are loaded with
 // wave-uniform addresses -> scalar loads (SGPR operands, no VGPR/LDS traffic).
 // Roots: with q = -(hb + sign(hb) sqrt(disc)) they are c/q and q/a; c/q is
-// the nearer one whenever hb < 0, so one division per candidate and the far
-// root q/a only when the near one is < eps.  Two exact culls skip spheres that
-// cannot win without the sqrt/division (DESIGN.md "scene scan"):
-//   hb >= 0 && c >= 0                      both roots <= 0
-//   hb < 0 && c > 0 && c >= tb*2|hb|*(1+2^-20)  near root c/q > tb (q <= 2|hb|(1+3u))
+// the nearer one whenever hb < 0, the far root q/a matters only when the near
+// one is < eps.  Roots stay fractions num/den (den > 0): "root < eps" is
+// num < eps*den, "nearer" is num*bq < bn*den, and one division per segment
+// turns the winner into t.  Two culls skip spheres that cannot win without
+// the sqrt (DESIGN.md "scene scan"):
+//   hb >= 0 && c >= 0                             both roots <= 0
+//   hb < 0 && c > 0 && c*bq >= bn*2|hb|*(1+2^-20)  near root not nearer (q <= 2|hb|(1+3u))
 constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20
 
 __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *__restrict__ geo, f3 o, f3 d, float &tbest)
 {
+    // the nearest root is kept as a fraction bn/bq (bq > 0); candidates are
+    // compared by cross-multiplication, only the winner is divided
     float a = dot3(d, d);
-    float tb = kInf;
+    float bn = kInf, bq = 1.0f;
     int id = -1;
     for (int i = 0; i < A.n; ++i) {
         float4 g0 = geo[i].g0;
@@ -140,37 +147,37 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *__restri
         }
         if (hb >= 0.0f && c >= 0.0f)
             continue;
-        if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * kCullMargin)
+        if (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * kCullMargin)
             continue;
         float disc = __builtin_fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
         float sq = sqrt_d(disc);
-        float root;
+        float num, den;
         if (hb < 0.0f) {
-            float q = sq - hb;
-#ifdef PTG_RCP  // speed probe only
-            root = c * (1.0f / q);
-#else
-            root = c / q;
-#endif
-            if (root < kEps) {
-                root = q / a;
-                if (root < kEps)
+            float q = sq - hb;  // > 0; roots c/q (near) and q/a (far)
+            num = c;
+            den = q;
+            if (c < kEps * q) {  // near root < eps
+                num = q;
+                den = a;
+                if (q < kEps * a)
                     continue;
             }
         } else {
-            float q = -(hb + sq);
-            root = c / q;
-            if (!(root >= kEps))
+            float qn = hb + sq;  // > 0 here (c < 0): root c/-qn
+            num = -c;
+            den = qn;
+            if (num < kEps * den)
                 continue;
         }
-        if (root < tb) {
-            tb = root;
+        if (num * bq < bn * den) {
+            bn = num;
+            bq = den;
             id = i;
         }
     }
-    tbest = tb;
+    tbest = id >= 0 ? bn / bq : kInf;
     return id;
 }
 
@@ -372,26 +379,38 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         start(item);
     int next = total < 64 ? total : 64;  // wave-uniform pool cursor
     // flat loop: one iteration = one bounce segment for every live lane
-    while (__ballot(item >= 0) != 0ull) {
-        bool done = false;
+    // flat loop: one iteration = one bounce segment for every live lane.  A
+    // finished lane waits until PTG_RESTART_BATCH lanes are waiting (or none
+    // is live, or the pool is empty), then the waiting lanes take the next
+    // unstarted paths together -- fewer, fuller executions of the restart code.
+    bool waiting = false;
+    for (;;) {
+        if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+            break;
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            done = segment(A, o, d, T, E, depth, st);
-            if (done) {
+            if (segment(A, o, d, T, E, depth, st)) {
                 atomicAdd(&lds_acc[wv][slot], quant(E.x));
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
                 atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
+                item = -1;
+                waiting = true;
             }
         }
-        const unsigned long long dm = __ballot(done);
-        if (done) {
-            int ni = next + (int)__popcll(dm & ((1ull << lane) - 1ull));
-            item = ni < total ? ni : -1;
-            if (item >= 0)
-                start(item);
+        const unsigned long long wm = __ballot(waiting);
+        const int nw = (int)__popcll(wm);
+        if (nw > 0 && (nw >= PTG_RESTART_BATCH || __ballot(item >= 0) == 0ull || next >= total)) {
+            if (waiting) {
+                int ni = next + (int)__popcll(wm & ((1ull << lane) - 1ull));
+                if (ni < total) {
+                    item = ni;
+                    start(item);
+                }
+                waiting = false;
+            }
+            next += nw;
         }
-        next += (int)__popcll(dm);
     }
     if constexpr (kCount) {
         unsigned long long ws = segs;

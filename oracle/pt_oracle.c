@@ -663,8 +663,10 @@ static void sincos2pi_B(float u, float *c, float *s)
 #define CULL_MARGIN 0x1.00001p+0f /* 1 + 2^-20 */
 static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
 {
+    /* nearest root kept as a fraction bn/bq (bq > 0): candidates are compared
+     * by cross-multiplication and only the winner is divided */
     float a = fdot(d, d);
-    float tb = INFF;
+    float bn = INFF, bq = 1.0f;
     int id = -1;
     for (int i = 0; i < n; ++i) {
         const sphB *sp = &s[i];
@@ -681,35 +683,39 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
         }
         if (hb >= 0.0f && c >= 0.0f)
             continue; /* both roots <= 0 */
-        if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * CULL_MARGIN)
-            continue; /* near root provably > tb */
+        if (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * CULL_MARGIN)
+            continue; /* near root provably not nearer than bn/bq */
         float disc = fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
         float sq = sqrt_B(disc);
-        float root;
+        float num, den;
         if (hb < 0.0f) {
-            float q = sq - hb;
-            root = c / q;
-            if (root < EPSF) {
-                root = q / a;
-                if (root < EPSF)
+            float q = sq - hb; /* > 0; roots c/q (near) and q/a (far) */
+            num = c;
+            den = q;
+            if (c < EPSF * q) { /* near root < eps */
+                num = q;
+                den = a;
+                if (q < EPSF * a)
                     continue;
             }
         } else {
-            float q = -(hb + sq);
-            root = c / q;
-            if (!(root >= EPSF))
+            float qn = hb + sq; /* > 0 here (c < 0): root c/-qn */
+            num = -c;
+            den = qn;
+            if (num < EPSF * den)
                 continue;
         }
-        if (root < tb) {
-            tb = root;
+        if (num * bq < bn * den) {
+            bn = num;
+            bq = den;
             id = i;
         }
     }
-    *tout = tb;
+    *tout = id >= 0 ? bn / bq : INFF;
     *idout = id;
-    return tb < INFF;
+    return id >= 0;
 }
 
 static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y, int sx, int sy,
