@@ -219,58 +219,65 @@ __device__ __forceinline__ bool segment(const KArgs &A, f3 &o, f3 &d, f3 &T, f3 
         col = S.s2;
     }
     T = mk3(T.x * col.x, T.y * col.y, T.z * col.z);
-    int mat = __float_as_int(s1.w);
-    bool spec = mat == PTG_SPECULAR;
-    if (mat == PTG_DIFFUSE) {  // main.cpp:44-58
+    // BRDF samplers (main.cpp:44-97).  Diffuse and dielectric lanes share the
+    // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
+    // holding both materials issues them once; every lane's arithmetic is the
+    // same as the per-material code (oracle sample_B).
+    const int mat = __float_as_int(s1.w);
+    const bool isD = mat == PTG_DIFFUSE;
+    const bool isG = mat == PTG_DIELECTRIC;
+    float cp = 0.0f, sp = 0.0f, ra = 0.0f;
+    if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
         float u_phi = draw(st);
-        float ra = draw(st);
-        float cp, sp;
+        ra = draw(st);
         sincos2pi(u_phi, cp, sp);
-        float sth = sqrt_d(ra);
-        float cth = sqrt_d(1.0f - ra);
-        f3 w = nn;
-        f3 uu = __builtin_fabsf(w.x) > 0.1f ? mk3(w.z, 0.0f, -w.x) : mk3(0.0f, -w.z, w.y);
-        uu = norm3(uu);
-        f3 vv = cross3(w, uu);
-        float cs = cp * sth, ss = sp * sth;
-        f3 nd = mk3(__builtin_fmaf(w.x, cth, __builtin_fmaf(vv.x, ss, uu.x * cs)),
-                    __builtin_fmaf(w.y, cth, __builtin_fmaf(vv.y, ss, uu.y * cs)),
-                    __builtin_fmaf(w.z, cth, __builtin_fmaf(vv.z, ss, uu.z * cs)));
-        o = p;
-        d = nd;  // unit by construction (main.cpp:55 re-normalises it)
-    } else if (mat == PTG_DIELECTRIC) {  // main.cpp:69-97
-        float ratio = front ? 0.5f : 2.0f;
-        f3 ud = norm3(d);
-        float x0 = -dot3(ud, nn);
-        float cth = 1.0f < x0 ? 1.0f : x0;
-        float sth = sqrt_d(__builtin_fmaf(-cth, cth, 1.0f));
-        bool reflect = ratio * sth > 1.0f;  // cannot refract: no Fresnel draw
+    }
+    // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
+    f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
+    f3 v1 = isD ? uu : d;
+    const float r1 = rsqrt_d(dot3(v1, v1));
+    v1 = mk3(v1.x * r1, v1.y * r1, v1.z * r1);
+    const float x0 = -dot3(v1, nn);
+    const float cthG = 1.0f < x0 ? 1.0f : x0;  // main.cpp:77
+    // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
+    const float s2 = sqrt_d(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
+    const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
+    bool spec = mat == PTG_SPECULAR;
+    if (isG) {
+        bool reflect = ratio * s2 > 1.0f;  // cannot refract: no Fresnel draw (main.cpp:89)
         if (!reflect) {
             const float r0 = 0x1.c71c74p-4f;  // ((1-ratio)/(1+ratio))^2, equal for ratio 0.5 and 2
-            float xm = 1.0f - cth;
+            float xm = 1.0f - cthG;
             float x2 = xm * xm;
             float x5 = (x2 * x2) * xm;
             float R = __builtin_fmaf(1.0f - r0, x5, r0);
             reflect = R > draw(st);
         }
-        if (reflect) {
-            spec = true;
-        } else {
-            f3 perp = mk3(__builtin_fmaf(nn.x, cth, ud.x) * ratio, __builtin_fmaf(nn.y, cth, ud.y) * ratio,
-                          __builtin_fmaf(nn.z, cth, ud.z) * ratio);
-            float sq = sqrt_d(__builtin_fabsf(1.0f - dot3(perp, perp)));
-            o = p;
-            d = mk3(__builtin_fmaf(nn.x, -sq, perp.x), __builtin_fmaf(nn.y, -sq, perp.y),
-                    __builtin_fmaf(nn.z, -sq, perp.z));
-        }
+        spec = reflect;
+    }
+    // op3: diffuse -> cos theta = sqrt(1 - r); dielectric -> |r_out_parallel| (main.cpp:94)
+    const f3 perp = mk3(__builtin_fmaf(nn.x, cthG, v1.x) * ratio, __builtin_fmaf(nn.y, cthG, v1.y) * ratio,
+                        __builtin_fmaf(nn.z, cthG, v1.z) * ratio);
+    const float s3 = sqrt_d(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));
+    f3 nd;
+    if (isD) {  // main.cpp:53-55 (unit by construction, not re-normalised)
+        f3 vv = cross3(nn, v1);
+        float cs = cp * s2, ss = sp * s2;
+        nd = mk3(__builtin_fmaf(nn.x, s3, __builtin_fmaf(vv.x, ss, v1.x * cs)),
+                 __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
+                 __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
+    } else {  // refraction, main.cpp:93-96
+        nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
+                 __builtin_fmaf(nn.z, -s3, perp.z));
     }
     if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
         float k = dot3(on, d);
         k = k + k;
         (void)draw(st);
-        o = p;
-        d = mk3(__builtin_fmaf(-k, on.x, d.x), __builtin_fmaf(-k, on.y, d.y), __builtin_fmaf(-k, on.z, d.z));
+        nd = mk3(__builtin_fmaf(-k, on.x, d.x), __builtin_fmaf(-k, on.y, d.y), __builtin_fmaf(-k, on.z, d.z));
     }
+    o = p;
+    d = nd;
     depth += 1;
     return depth >= kDepthLimit;
 }
