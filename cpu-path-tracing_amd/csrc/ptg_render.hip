@@ -9,10 +9,11 @@
 //    roulette, depth cap) accumulates it and immediately starts its next
 //    sample (per-lane path regeneration), so the wave keeps ~all lanes busy
 //    despite the geometric path-length tail;
-//  * the scene scan reads sphere records with wave-uniform scalar loads
-//    (s_load into SGPRs -- the SMEM broadcast path, no VGPRs or LDS cycles
-//    spent on the 8-sphere scenes) or, with PTG_SPHERES_LDS, stages them in
-//    LDS once per workgroup;
+//  * sphere geometry records are staged in LDS once per workgroup and read
+//    with uniform-address (broadcast) LDS loads in the scan (up to 256
+//    spheres; measured 1.5 % faster than scalar loads, 7 % faster than
+//    software-prefetched scalar loads); larger scenes use wave-uniform scalar
+//    loads (s_load into SGPRs) from L2/HBM;
 //  * per-wave segment counts via ballot popcount, one atomic per wave;
 //  * sub-pixel combine by in-register cross-lane reads, then coalesced
 //    192-B stores (three lanes of each pixel write R, G, B).
@@ -48,6 +49,7 @@ int fail(int code, const std::string &msg)
     } while (0)
 
 constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kMaxLdsSpheres = 256;  // 8 KB of geometry per workgroup; 8 workgroups/CU fit 160 KB LDS
 #ifndef PTG_RESTART_BATCH
 #define PTG_RESTART_BATCH 8  // measured: 8 beats 1, 4, 16 (profiles/)
 #endif
@@ -124,16 +126,26 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 //   hb < 0 && c > 0 && c*bq >= bn*2|hb|*(1+2^-20)  near root not nearer (q <= 2|hb|(1+3u))
 constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20
 
-__device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *__restrict__ geo, f3 o, f3 d, float &tbest)
+__device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
 {
     // the nearest root is kept as a fraction bn/bq (bq > 0); candidates are
     // compared by cross-multiplication, only the winner is divided
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     int id = -1;
+#ifdef PTG_PREFETCH
+    float4 n0 = geo[0].g0, n1 = geo[0].g1;  // scalar loads one sphere ahead
+#endif
     for (int i = 0; i < A.n; ++i) {
+#ifdef PTG_PREFETCH
+        const float4 g0 = n0, g1 = n1;
+        const int ip = i + 1 < A.n ? i + 1 : i;
+        n0 = geo[ip].g0;
+        n1 = geo[ip].g1;
+#else
         float4 g0 = geo[i].g0;
         float4 g1 = geo[i].g1;
+#endif
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
         float ed = dot3(e, d);
         float ee = dot3(e, e);
@@ -184,10 +196,11 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *__restri
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
-__device__ __forceinline__ bool segment(const KArgs &A, f3 &o, f3 &d, f3 &T, f3 &E, int &depth, uint32_t &st)
+__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o, f3 &d, f3 &T, f3 &E, int &depth,
+                                        uint32_t &st)
 {
     float t;
-    int id = scene_scan(A, A.geo, o, d, t);
+    int id = scene_scan(A, geo, o, d, t);
     if (id < 0) {  // main.cpp:115-120: sky
         f3 ud = norm3(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -312,12 +325,23 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // so all lanes stay busy until the pool is empty.  Path radiance is
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
-template <bool kCount>
+template <bool kCount, bool kLdsGeo>
 __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
     __shared__ unsigned long long lds_acc[kWavesPerBlock][64 * 3];
     __shared__ unsigned long long lds_key[kWavesPerBlock][64];
     __shared__ uint32_t lds_pix[kWavesPerBlock][64];  // slot -> x | sx << 20 | sy << 26
+    // sphere geometry staged once per workgroup in LDS (uniform-address
+    // ds_read_b128 broadcasts in the scan); larger scenes read it with
+    // wave-uniform scalar loads from HBM/L2 instead
+    __shared__ GeoRec lds_geo[kLdsGeo ? kMaxLdsSpheres : 1];
+    const GeoRec *geo = A.geo;
+    if constexpr (kLdsGeo) {
+        for (int i = threadIdx.x; i < A.n; i += kBlock)
+            lds_geo[i] = A.geo[i];
+        __syncthreads();
+        geo = lds_geo;
+    }
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler keep all
     // per-unit bookkeeping in SGPRs
@@ -397,7 +421,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            if (segment(A, o, d, T, E, depth, st)) {
+            if (segment(A, geo, o, d, T, E, depth, st)) {
                 atomicAdd(&lds_acc[wv][slot], quant(E.x));
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
                 atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
@@ -428,18 +452,35 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (lane < nv) {
+    if (A.single_chunk) {
+        // the unit holds every sample of its pixels: resolve in the wave
+        // (main.cpp:195-196, same arithmetic as resolve_kernel) and write
+        // 12 B per pixel -- the only HBM traffic of the frame
+        if (lane < npix && r < A.H) {
+            f3 pix = mk3(0.0f, 0.0f, 0.0f);
+            for (int j = 0; j < A.lanes_per_pixel; ++j) {
+                const int sl = lane * A.lanes_per_pixel + j;
+                float m[3];
+                for (int c = 0; c < 3; ++c) {
+                    const unsigned long long sum = lds_acc[wv][sl + 64 * c];
+                    const float mean = A.samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)A.samps) : 0.0f;
+                    m[c] = mean < 0.0f ? 0.0f : (1.0f < mean ? 1.0f : mean);
+                }
+                pix = mk3(__builtin_fmaf(m[0], A.inv_sub2, pix.x), __builtin_fmaf(m[1], A.inv_sub2, pix.y),
+                          __builtin_fmaf(m[2], A.inv_sub2, pix.z));
+            }
+            float *out = A.out + ((size_t)slab_row * A.W + x0 + lane) * 3;
+            out[0] = pix.x;
+            out[1] = pix.y;
+            out[2] = pix.z;
+        }
+    } else if (lane < nv) {
+        // several units share these pixels: exact u64 adds, resolved later
         unsigned long long *g = A.acc + (((size_t)slab_row * A.W + x0) * A.lanes_per_pixel + lane) * 3;
         unsigned long long vx = lds_acc[wv][lane], vy = lds_acc[wv][lane + 64], vz = lds_acc[wv][lane + 128];
-        if (A.single_chunk) {  // sole writer of these sums: plain stores
-            g[0] = vx;
-            g[1] = vy;
-            g[2] = vz;
-        } else {
-            if (vx) atomicAdd(g + 0, vx);
-            if (vy) atomicAdd(g + 1, vy);
-            if (vz) atomicAdd(g + 2, vz);
-        }
+        if (vx) atomicAdd(g + 0, vx);
+        if (vy) atomicAdd(g + 1, vy);
+        if (vz) atomicAdd(g + 2, vz);
     }
 }
 
@@ -496,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     bool done = false;
     while (!done) {
         segs += 1;
-        done = segment(A, o, d, T, E, depth, st);
+        done = segment(A, A.geo, o, d, T, E, depth, st);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -784,7 +825,7 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     int grid = 0;
     fill_launch(ctx, params, A, grid);
     // exact accumulator: allocated (zeroed) on first use at a size, kept zero by resolve_kernel
-    size_t need = (size_t)A.slab_rows * A.W * A.lanes_per_pixel * 3;
+    size_t need = (A.single_chunk && grid > 0) ? 0 : (size_t)A.slab_rows * A.W * A.lanes_per_pixel * 3;
     if (need > ctx->acc_elems) {
         if (ctx->d_acc)
             PTG_HIP(hipFree(ctx->d_acc));
@@ -800,15 +841,18 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     A.segments = d_segments;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (grid > 0) {
+        const bool lds = A.n <= kMaxLdsSpheres;
         if (d_segments)
-            render_kernel<true><<<grid, kBlock, 0, s>>>(A);
+            lds ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, 0, s>>>(A);
         else
-            render_kernel<false><<<grid, kBlock, 0, s>>>(A);
+            lds ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, 0, s>>>(A);
         PTG_HIP(hipGetLastError());
     }
-    long long pixels = (long long)A.slab_rows * A.W;
-    resolve_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>(A);
-    PTG_HIP(hipGetLastError());
+    if (!A.single_chunk || grid == 0) {  // several units per pixel, or no samples at all
+        long long pixels = (long long)A.slab_rows * A.W;
+        resolve_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>(A);
+        PTG_HIP(hipGetLastError());
+    }
     return PTG_OK;
 }
 
