@@ -49,7 +49,10 @@ int fail(int code, const std::string &msg)
     } while (0)
 
 constexpr int kBlock = 256;        // 4 waves per workgroup
-constexpr int kMaxLdsSpheres = 256;  // 8 KB of geometry per workgroup; 8 workgroups/CU fit 160 KB LDS
+#ifndef PTG_MAX_LDS_SPHERES
+#define PTG_MAX_LDS_SPHERES 256
+#endif
+constexpr int kMaxLdsSpheres = PTG_MAX_LDS_SPHERES;  // 8 KB of geometry per workgroup; 8 workgroups/CU fit 160 KB LDS
 #ifndef PTG_RESTART_BATCH
 #define PTG_RESTART_BATCH 8  // measured: 8 beats 1, 4, 16 (profiles/)
 #endif
@@ -75,6 +78,8 @@ struct KArgs {
     float invW, invH, inv_samps, sub_len, inv_sub2;
     unsigned long long seed;
     int chunk, n_groups, single_chunk;
+    int sample_begin, sample_end;  // samples [begin, end) of every sub-pixel in this launch
+    int keep_acc;                  // resolve without re-zeroing (progressive previews)
     long long n_units;
     float *out;
     unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
@@ -196,8 +201,8 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
-__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o, f3 &d, f3 &T, f3 &E, int &depth,
-                                        uint32_t &st)
+__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const ShadeRec *shade, f3 &o, f3 &d, f3 &T,
+                                        f3 &E, int &depth, uint32_t &st)
 {
     float t;
     int id = scene_scan(A, geo, o, d, t);
@@ -210,7 +215,7 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, f3 &o
                 __builtin_fmaf(T.z, __builtin_fmaf(tt, 1.0f, it), E.z));
         return true;
     }
-    const ShadeRec &S = A.shade[id];
+    const ShadeRec &S = shade[id];
     float4 s0 = S.s0, s1 = S.s1;
     // hit_record.cpp:3-12
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
@@ -336,11 +341,22 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     // wave-uniform scalar loads from HBM/L2 instead
     __shared__ GeoRec lds_geo[kLdsGeo ? kMaxLdsSpheres : 1];
     const GeoRec *geo = A.geo;
+    const ShadeRec *shade = A.shade;
+#ifdef PTG_SHADE_LDS
+    __shared__ ShadeRec lds_shade[kLdsGeo ? kMaxLdsSpheres : 1];
+#endif
     if constexpr (kLdsGeo) {
-        for (int i = threadIdx.x; i < A.n; i += kBlock)
+        for (int i = threadIdx.x; i < A.n; i += kBlock) {
             lds_geo[i] = A.geo[i];
+#ifdef PTG_SHADE_LDS
+            lds_shade[i] = A.shade[i];
+#endif
+        }
         __syncthreads();
         geo = lds_geo;
+#ifdef PTG_SHADE_LDS
+        shade = lds_shade;
+#endif
     }
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler keep all
@@ -359,8 +375,8 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     int npix = A.W - x0;
     npix = npix < A.pixels_per_wave ? npix : A.pixels_per_wave;
     const int nv = r < A.H ? npix * A.lanes_per_pixel : 0;  // valid slots are a prefix
-    const int s0 = chunk * A.chunk;
-    int cnt = A.samps - s0;
+    const int s0 = A.sample_begin + chunk * A.chunk;
+    int cnt = A.sample_end - s0;
     cnt = cnt < A.chunk ? cnt : A.chunk;
     const int total = nv * cnt;
 
@@ -421,7 +437,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            if (segment(A, geo, o, d, T, E, depth, st)) {
+            if (segment(A, geo, shade, o, d, T, E, depth, st)) {
                 atomicAdd(&lds_acc[wv][slot], quant(E.x));
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
                 atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
@@ -500,7 +516,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(KArgs A)
         float m[3];
         for (int c = 0; c < 3; ++c) {
             unsigned long long sum = g[3 * j + c];
-            g[3 * j + c] = 0ull;
+            if (!A.keep_acc)
+                g[3 * j + c] = 0ull;
             float mean = A.samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)A.samps) : 0.0f;
             m[c] = mean < 0.0f ? 0.0f : (1.0f < mean ? 1.0f : mean);
         }
@@ -537,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     bool done = false;
     while (!done) {
         segs += 1;
-        done = segment(A, A.geo, o, d, T, E, depth, st);
+        done = segment(A, A.geo, A.shade, o, d, T, E, depth, st);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -664,8 +681,13 @@ int check_params(const ptg_params *p)
     return PTG_OK;
 }
 
-void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid)
+// Launch geometry for samples [s_begin, s_end) of every sub-pixel.
+void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid, int s_begin = 0, int s_end = -1,
+                 bool accumulate_only = false)
 {
+    if (s_end < 0)
+        s_end = p->samples;
+    const int nsamp = s_end - s_begin;
     A = ctx->base;
     A.W = p->width;
     A.H = p->height;
@@ -685,22 +707,26 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     A.sub_len = 1.0f / (float)p->num_subpixels;
     A.inv_sub2 = 1.0f / (float)(p->num_subpixels * p->num_subpixels);
     A.seed = p->seed;
-    // work unit = pixel group x chunk of samples (auto: 32 samples per sub-pixel)
-    // auto: split the samples only as far as needed for ~96k work units (about
-    // 16 waves per SIMD slot on 256 CUs), which keeps the grid-level tail small
+    A.sample_begin = s_begin;
+    A.sample_end = s_end;
+    A.keep_acc = 0;
+    // work unit = pixel group x chunk of samples.  Auto: split the samples
+    // only as far as needed for ~96k work units (about 16 waves per SIMD slot
+    // on 256 CUs), which keeps the grid-level tail small at any GPU count.
     const int groups = A.slab_rows * A.waves_per_row;
     int chunk = p->chunk_samples;
     if (chunk <= 0) {
         long long want = (98304 + groups - 1) / groups;
-        long long nch = want < 1 ? 1 : (want > p->samples ? p->samples : want);
-        chunk = nch > 0 ? (int)((p->samples + nch - 1) / nch) : 1;
+        long long nch = want < 1 ? 1 : (want > nsamp ? nsamp : want);
+        chunk = nch > 0 ? (int)((nsamp + nch - 1) / nch) : 1;
     }
-    if (chunk > p->samples)
-        chunk = p->samples > 0 ? p->samples : 1;
+    if (chunk > nsamp)
+        chunk = nsamp > 0 ? nsamp : 1;
     A.chunk = chunk;
-    A.n_groups = A.slab_rows * A.waves_per_row;
-    int n_chunks = p->samples > 0 ? (p->samples + chunk - 1) / chunk : 0;
-    A.single_chunk = n_chunks <= 1;
+    A.n_groups = groups;
+    int n_chunks = nsamp > 0 ? (nsamp + chunk - 1) / chunk : 0;
+    // in-wave resolve only when one unit holds ALL samples of its pixels
+    A.single_chunk = !accumulate_only && n_chunks <= 1 && s_begin == 0 && s_end == p->samples;
     A.n_units = (long long)A.n_groups * n_chunks;
     grid = (int)((A.n_units + kWavesPerBlock - 1) / kWavesPerBlock);
 }
@@ -812,6 +838,54 @@ int ptg_context_destroy(ptg_context *ctx)
     return PTG_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// exact accumulator: allocated (zeroed) on first use at a size; resolve_kernel
+// keeps it zero between one-shot frames
+int ensure_acc(ptg_context *ctx, size_t need)
+{
+    if (need <= ctx->acc_elems)
+        return PTG_OK;
+    if (ctx->d_acc)
+        PTG_HIP(hipFree(ctx->d_acc));
+    ctx->d_acc = nullptr;
+    ctx->acc_elems = 0;
+    if (hipMalloc(&ctx->d_acc, need * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the accumulator failed");
+    PTG_HIP(hipMemset(ctx->d_acc, 0, need * sizeof(unsigned long long)));
+    ctx->acc_elems = need;
+    return PTG_OK;
+}
+
+size_t acc_elems_for(const KArgs &A) { return (size_t)A.slab_rows * A.W * A.lanes_per_pixel * 3; }
+
+int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
+{
+    if (grid <= 0)
+        return PTG_OK;
+    const bool lds = A.n <= kMaxLdsSpheres;
+    if (count)
+        lds ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, 0, s>>>(A);
+    else
+        lds ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, 0, s>>>(A);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int launch_resolve(const KArgs &A, hipStream_t s)
+{
+    long long pixels = (long long)A.slab_rows * A.W;
+    resolve_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>(A);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab, unsigned long long *d_segments,
                       void *stream)
 {
@@ -824,35 +898,76 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     KArgs A;
     int grid = 0;
     fill_launch(ctx, params, A, grid);
-    // exact accumulator: allocated (zeroed) on first use at a size, kept zero by resolve_kernel
-    size_t need = (A.single_chunk && grid > 0) ? 0 : (size_t)A.slab_rows * A.W * A.lanes_per_pixel * 3;
-    if (need > ctx->acc_elems) {
-        if (ctx->d_acc)
-            PTG_HIP(hipFree(ctx->d_acc));
-        ctx->d_acc = nullptr;
-        ctx->acc_elems = 0;
-        if (hipMalloc(&ctx->d_acc, need * sizeof(unsigned long long)) != hipSuccess)
-            return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the accumulator failed");
-        PTG_HIP(hipMemset(ctx->d_acc, 0, need * sizeof(unsigned long long)));
-        ctx->acc_elems = need;
-    }
+    const bool resolve = !A.single_chunk || grid == 0;  // several units per pixel, or no samples at all
+    if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
+        return rc;
     A.out = d_slab;
     A.acc = ctx->d_acc;
     A.segments = d_segments;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (grid > 0) {
-        const bool lds = A.n <= kMaxLdsSpheres;
-        if (d_segments)
-            lds ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, 0, s>>>(A);
-        else
-            lds ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, 0, s>>>(A);
-        PTG_HIP(hipGetLastError());
-    }
-    if (!A.single_chunk || grid == 0) {  // several units per pixel, or no samples at all
-        long long pixels = (long long)A.slab_rows * A.W;
-        resolve_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>(A);
-        PTG_HIP(hipGetLastError());
-    }
+    if ((rc = launch_render(A, grid, d_segments != nullptr, s)))
+        return rc;
+    return resolve ? launch_resolve(A, s) : PTG_OK;
+}
+
+int ptg_accumulate_device(ptg_context *ctx, const ptg_params *params, int32_t sample_begin, int32_t sample_end,
+                          unsigned long long *d_segments, void *stream)
+{
+    if (!ctx)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL context");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    if (sample_begin < 0 || sample_end < sample_begin || sample_end > params->samples)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "sample range must satisfy 0 <= begin <= end <= samples");
+    PTG_HIP(hipSetDevice(ctx->device));
+    KArgs A;
+    int grid = 0;
+    fill_launch(ctx, params, A, grid, sample_begin, sample_end, /*accumulate_only=*/true);
+    if ((rc = ensure_acc(ctx, acc_elems_for(A))))
+        return rc;
+    A.acc = ctx->d_acc;
+    A.segments = d_segments;
+    return launch_render(A, grid, d_segments != nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+int ptg_resolve_device(ptg_context *ctx, const ptg_params *params, int32_t samples_done, float *d_slab, void *stream)
+{
+    if (!ctx || !d_slab)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL context or output");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    if (samples_done < 0 || samples_done > params->samples)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "samples_done must be in [0, samples]");
+    PTG_HIP(hipSetDevice(ctx->device));
+    KArgs A;
+    int grid = 0;
+    fill_launch(ctx, params, A, grid);
+    if ((rc = ensure_acc(ctx, acc_elems_for(A))))
+        return rc;
+    A.samps = samples_done;  // mean over the samples accumulated so far
+    A.keep_acc = 1;
+    A.acc = ctx->d_acc;
+    A.out = d_slab;
+    return launch_resolve(A, reinterpret_cast<hipStream_t>(stream));
+}
+
+int ptg_reset_accumulation_device(ptg_context *ctx, const ptg_params *params, void *stream)
+{
+    if (!ctx)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL context");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    PTG_HIP(hipSetDevice(ctx->device));
+    KArgs A;
+    int grid = 0;
+    fill_launch(ctx, params, A, grid);
+    if ((rc = ensure_acc(ctx, acc_elems_for(A))))
+        return rc;
+    PTG_HIP(hipMemsetAsync(ctx->d_acc, 0, acc_elems_for(A) * sizeof(unsigned long long),
+                           reinterpret_cast<hipStream_t>(stream)));
     return PTG_OK;
 }
 

@@ -18,6 +18,7 @@ EXPORTS = (
     "ptg_abi_version", "ptg_last_error", "ptg_device_count", "ptg_render",
     "ptg_context_create", "ptg_context_destroy", "ptg_shard_rows", "ptg_render_device",
     "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
+    "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device",
 )
 
 
@@ -58,6 +59,9 @@ def lib():
             "ptg_unshard_device": (I, [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
             "ptg_tonemap_device": (I, [P, P, C.c_size_t, P]),
             "ptg_trace_samples_device": (I, [P, C.POINTER(Params), P, C.c_size_t, P, P, P]),
+            "ptg_reset_accumulation_device": (I, [P, C.POINTER(Params), P]),
+            "ptg_accumulate_device": (I, [P, C.POINTER(Params), C.c_int32, C.c_int32, P, P]),
+            "ptg_resolve_device": (I, [P, C.POINTER(Params), C.c_int32, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

@@ -136,6 +136,29 @@ class Context:
                                       C.c_void_p(segments.data_ptr()) if segments is not None else None,
                                       C.c_void_p(s)), "ptg_render_device")
 
+    # ---- progressive accumulation (ptg_accumulate_device / ptg_resolve_device)
+    def reset_accumulation(self, params: Params, stream=None) -> None:
+        import torch
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        check(lib().ptg_reset_accumulation_device(self._h, C.byref(params), C.c_void_p(s)), "ptg_reset_accumulation_device")
+
+    def accumulate(self, params: Params, sample_begin: int, sample_end: int, segments=None, stream=None) -> None:
+        """Add samples [sample_begin, sample_end) of every sub-pixel."""
+        import torch
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        check(lib().ptg_accumulate_device(self._h, C.byref(params), int(sample_begin), int(sample_end),
+                                          C.c_void_p(segments.data_ptr()) if segments is not None else None,
+                                          C.c_void_p(s)), "ptg_accumulate_device")
+
+    def resolve(self, out, params: Params, samples_done: int, stream=None) -> None:
+        """Preview/final image from the samples accumulated so far."""
+        import torch
+        _check_tensor(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
+                      * params.width * 3)
+        s = (stream or torch.cuda.current_stream(out.device)).cuda_stream
+        check(lib().ptg_resolve_device(self._h, C.byref(params), int(samples_done), C.c_void_p(out.data_ptr()),
+                                       C.c_void_p(s)), "ptg_resolve_device")
+
     def trace_samples(self, coords, params: Params):
         """Parity probe: radiance + segment count of individual paths
         (coords: int32 CUDA tensor [n, 5] = x, y, sx, sy, sample)."""

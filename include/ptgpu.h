@@ -119,6 +119,19 @@ int ptg_shard_rows(int32_t height, int32_t band_rows, int32_t shard_count, int32
 int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
                       unsigned long long *d_segments, void *stream);
 
+/* ---- progressive accumulation (README.md:9 "make the rendering process
+ * progressive") ----------------------------------------
+ * Sample passes add exact per-sub-pixel sums into the context's accumulator;
+ * a resolve turns the sums so far into an image (clamped means over
+ * samples_done samples) without consuming them.  After passes that together
+ * cover samples [0, params->samples), ptg_resolve_device(..., samples, ...)
+ * equals ptg_render_device bit for bit.  Reset before a new frame. */
+int ptg_reset_accumulation_device(ptg_context *ctx, const ptg_params *params, void *stream);
+int ptg_accumulate_device(ptg_context *ctx, const ptg_params *params, int32_t sample_begin, int32_t sample_end,
+                          unsigned long long *d_segments, void *stream);
+int ptg_resolve_device(ptg_context *ctx, const ptg_params *params, int32_t samples_done, float *d_slab,
+                       void *stream);
+
 /* Reassemble shard_count gathered slabs (rank-major, as all-gather lays them
  * out) into the width*height*3 image. */
 int ptg_unshard_device(const float *d_gathered, float *d_image, int32_t width, int32_t height,

@@ -207,3 +207,30 @@ def test_invalid_arguments_fail_loudly():
         ptgpu.render(scn, cam, img, 8, 8, 4, num_subpixels=9)
     with pytest.raises(ptgpu.PtgError):
         ptgpu.render(scn, cam, img, 8, 8, -1)
+
+
+def test_progressive_accumulation_matches_one_shot():
+    """f2 (README.md:9): sample passes into the exact accumulator; a preview
+    after k samples equals a k-sample render, the last resolve equals the
+    one-shot frame bit for bit."""
+    _require_gpu()
+    W, H, samps = 40, 24, 16
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    p = ptgpu.make_params(W, H, samps, 2, SEED)
+    rows = ptgpu.shard_rows(H, 8, 1)
+    out = torch.empty(rows * W * 3, dtype=torch.float32, device="cuda")
+    sp, ca = _oracle_scene(scn, cam)
+    with ptgpu.Context(scn, cam) as ctx:
+        ctx.reset_accumulation(p)
+        done = 0
+        for end in (3, 10, 16):
+            ctx.accumulate(p, done, end)
+            done = end
+            ctx.resolve(out, p, done)
+            torch.cuda.synchronize()
+            img = out.cpu().numpy().reshape(rows, W, 3)[:H]
+            ref, _ = po.render_xs_f32(sp, ca, W, H, done, 2, SEED)
+            _check_equal(img, ref)
+        one, _ = _gpu_image(scn, cam, W, H, samps)
+        assert np.array_equal(img, one)
