@@ -50,9 +50,12 @@ int fail(int code, const std::string &msg)
 
 constexpr int kBlock = 256;        // 4 waves per workgroup
 #ifndef PTG_MAX_LDS_SPHERES
-#define PTG_MAX_LDS_SPHERES 256
+#define PTG_MAX_LDS_SPHERES 64
 #endif
-constexpr int kMaxLdsSpheres = PTG_MAX_LDS_SPHERES;  // 8 KB of geometry per workgroup; 8 workgroups/CU fit 160 KB LDS
+// scenes up to 64 spheres keep geometry (2 KB) and shading records (4 KB) in
+// LDS: 15 KB per workgroup, 8 workgroups per CU (measured: +1.3 % over
+// geometry-only staging of up to 256 spheres, which itself beat scalar loads)
+constexpr int kMaxLdsSpheres = PTG_MAX_LDS_SPHERES;
 #ifndef PTG_RESTART_BATCH
 #define PTG_RESTART_BATCH 8  // measured: 8 beats 1, 4, 16 (profiles/)
 #endif
@@ -336,27 +339,21 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     __shared__ unsigned long long lds_acc[kWavesPerBlock][64 * 3];
     __shared__ unsigned long long lds_key[kWavesPerBlock][64];
     __shared__ uint32_t lds_pix[kWavesPerBlock][64];  // slot -> x | sx << 20 | sy << 26
-    // sphere geometry staged once per workgroup in LDS (uniform-address
-    // ds_read_b128 broadcasts in the scan); larger scenes read it with
-    // wave-uniform scalar loads from HBM/L2 instead
+    // sphere records staged once per workgroup in LDS (uniform-address
+    // ds_read_b128 broadcasts in the scan, by-id gathers at hits); larger
+    // scenes read geometry with wave-uniform scalar loads from L2/HBM instead
     __shared__ GeoRec lds_geo[kLdsGeo ? kMaxLdsSpheres : 1];
     const GeoRec *geo = A.geo;
     const ShadeRec *shade = A.shade;
-#ifdef PTG_SHADE_LDS
     __shared__ ShadeRec lds_shade[kLdsGeo ? kMaxLdsSpheres : 1];
-#endif
     if constexpr (kLdsGeo) {
         for (int i = threadIdx.x; i < A.n; i += kBlock) {
             lds_geo[i] = A.geo[i];
-#ifdef PTG_SHADE_LDS
             lds_shade[i] = A.shade[i];
-#endif
         }
         __syncthreads();
         geo = lds_geo;
-#ifdef PTG_SHADE_LDS
         shade = lds_shade;
-#endif
     }
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler keep all
