@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/ptgpu.h"
+#include "bvh_build.hpp"
 #include "pt_device.hpp"
 
 using namespace ptg;
@@ -56,6 +57,11 @@ constexpr int kBlock = 256;        // 4 waves per workgroup
 // LDS: 15 KB per workgroup, 8 workgroups per CU (measured: +1.3 % over
 // geometry-only staging of up to 256 spheres, which itself beat scalar loads)
 constexpr int kMaxLdsSpheres = PTG_MAX_LDS_SPHERES;
+// nearest-hit rule and scan: <= kLinearMax spheres -> linear scan from LDS with
+// fraction comparisons; more -> BVH with the reference's per-candidate
+// division rule (DESIGN.md "scene scan"); the oracle switches at the same n
+constexpr int kLinearMax = 64;
+static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_RESTART_BATCH
 #define PTG_RESTART_BATCH 8  // measured: 8 beats 1, 4, 16 (profiles/)
 #endif
@@ -69,6 +75,13 @@ struct KArgs {
     const GeoRec *geo;
     const ShadeRec *shade;
     int n;
+    // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
+    const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
+    const GeoRec *bvh_geo;    // leaf-ordered geometry
+    const int *bvh_id;        // leaf-ordered scene indices
+    const GeoRec *big_geo;    // huge spheres, tested linearly
+    const int *big_id;
+    int n_nodes, n_big;
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
     float pos_x, pos_y, pos_z;
     float base_x, base_y, base_z;
@@ -201,14 +214,109 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
     return id;
 }
 
+// Scenes with more than kLinearMax spheres: the huge
+// spheres linearly, then a stackless walk of the BVH.  The nearest-hit rule
+// here is the reference's own -- every candidate root is divided,
+// t = fl(num/den), and the winner is the smallest t, lowest scene index on
+// ties (main.cpp:35 strict <, in index order) -- which does not depend on the
+// visiting order, so the oracle reproduces it with a linear scan.  Box tests
+// only cull: boxes are padded (bvh_build.hpp) and use fast reciprocals.
+__device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1, const int gid, const f3 o,
+                                                const f3 d, const float a, float &tb, int &id)
+{
+    f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
+    float ed = dot3(e, d);
+    float ee = dot3(e, e);
+    float hb, c;
+    if (g0.w >= 0.0f) {
+        hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
+        c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
+    } else {
+        hb = ed;
+        c = ee + g1.w;
+    }
+    if (hb >= 0.0f && c >= 0.0f)
+        return;
+    if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * kCullMargin)
+        return;  // near root > tb (exact, see scene_scan)
+    float disc = __builtin_fmaf(hb, hb, -(a * c));
+    if (disc < 0.0f)
+        return;
+    float sq = sqrt_d(disc);
+    float num, den;
+    if (hb < 0.0f) {
+        float q = sq - hb;
+        num = c;
+        den = q;
+        if (c < kEps * q) {
+            num = q;
+            den = a;
+            if (q < kEps * a)
+                return;
+        }
+    } else {
+        float qn = hb + sq;
+        num = -c;
+        den = qn;
+        if (num < kEps * den)
+            return;
+    }
+    const float t = num / den;
+    if (t < tb || (t == tb && gid < id)) {
+        tb = t;
+        id = gid;
+    }
+}
+
+__device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest)
+{
+    const float a = dot3(d, d);
+    float tb = kInf;
+    int id = -1;
+    for (int k = 0; k < A.n_big; ++k)
+        test_sphere_lex(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tb, id);
+    // slab test (culling only: fast reciprocals, padded boxes)
+    const float ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
+    const float iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
+    const float iz = d.z != 0.0f ? __builtin_amdgcn_rcpf(d.z) : __builtin_copysignf(1e30f, d.z);
+    const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
+    int ni = 0;
+    while (ni < A.n_nodes) {
+        const float4 n0 = A.bvh_nodes[2 * ni];
+        const float4 n1 = A.bvh_nodes[2 * ni + 1];
+        float tx1 = __builtin_fmaf(n0.x, ix, -ox), tx2 = __builtin_fmaf(n1.x, ix, -ox);
+        float ty1 = __builtin_fmaf(n0.y, iy, -oy), ty2 = __builtin_fmaf(n1.y, iy, -oy);
+        float tz1 = __builtin_fmaf(n0.z, iz, -oz), tz2 = __builtin_fmaf(n1.z, iz, -oz);
+        float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
+                                     __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
+        float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
+                                      __builtin_fminf(__builtin_fmaxf(tz1, tz2), tb * 1.0001f));
+        if (t_in > t_out * 1.0001f + 1e-6f) {
+            ni = __float_as_int(n0.w);  // skip the subtree
+            continue;
+        }
+        const int leaf = __float_as_int(n1.w);
+        if (leaf >= 0) {
+            const int first = leaf & 0xFFFFFF, cnt = leaf >> 24;
+            for (int j = 0; j < cnt; ++j)
+                test_sphere_lex(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d, a, tb,
+                                id);
+        }
+        ++ni;
+    }
+    tbest = tb;
+    return id;
+}
+
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
+template <bool kBvh>
 __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const ShadeRec *shade, f3 &o, f3 &d, f3 &T,
                                         f3 &E, int &depth, uint32_t &st)
 {
     float t;
-    int id = scene_scan(A, geo, o, d, t);
+    int id = kBvh ? scene_scan_bvh(A, o, d, t) : scene_scan(A, geo, o, d, t);
     if (id < 0) {  // main.cpp:115-120: sky
         f3 ud = norm3(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -333,7 +441,7 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // so all lanes stay busy until the pool is empty.  Path radiance is
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
-template <bool kCount, bool kLdsGeo>
+template <bool kCount, bool kBvh>
 __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
     __shared__ unsigned long long lds_acc[kWavesPerBlock][64 * 3];
@@ -342,6 +450,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     // sphere records staged once per workgroup in LDS (uniform-address
     // ds_read_b128 broadcasts in the scan, by-id gathers at hits); larger
     // scenes read geometry with wave-uniform scalar loads from L2/HBM instead
+    constexpr bool kLdsGeo = !kBvh;  // linear scenes (<= kMaxLdsSpheres) live in LDS
     __shared__ GeoRec lds_geo[kLdsGeo ? kMaxLdsSpheres : 1];
     const GeoRec *geo = A.geo;
     const ShadeRec *shade = A.shade;
@@ -434,7 +543,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            if (segment(A, geo, shade, o, d, T, E, depth, st)) {
+            if (segment<kBvh>(A, geo, shade, o, d, T, E, depth, st)) {
                 atomicAdd(&lds_acc[wv][slot], quant(E.x));
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
                 atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
@@ -528,6 +637,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(KArgs A)
 }
 
 // Parity probe: one path per record {x, y, sx, sy, sample}.
+template <bool kBvh>
 __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *coords, int n, float *out,
                                                          int32_t *segs_out)
 {
@@ -551,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     bool done = false;
     while (!done) {
         segs += 1;
-        done = segment(A, A.geo, A.shade, o, d, T, E, depth, st);
+        done = segment<kBvh>(A, A.geo, A.shade, o, d, T, E, depth, st);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -591,6 +701,7 @@ struct ptg_context {
     int n;
     GeoRec *d_geo;
     ShadeRec *d_shade;
+    void *d_bvh;  // one allocation: nodes | leaf geometry | leaf ids | big geometry | big ids
     unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
     size_t acc_elems;
     KArgs base;  // camera + scene fields filled
@@ -805,6 +916,38 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.geo = ctx->d_geo;
     A.shade = ctx->d_shade;
     A.n = (int)n_spheres;
+    if ((int)n_spheres > kLinearMax) {
+        BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);
+        const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();
+        const size_t off_geo = n_nodes * sizeof(BvhNodeHost);
+        const size_t off_id = off_geo + n_leaf * sizeof(GeoRec);
+        const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
+        const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
+        const size_t total = off_bid + n_big * sizeof(int) + 16;
+        std::vector<unsigned char> blob(total, 0);
+        std::memcpy(blob.data(), b.nodes.data(), off_geo);
+        for (size_t i = 0; i < n_leaf; ++i) {
+            std::memcpy(blob.data() + off_geo + i * sizeof(GeoRec), &geo[b.order[i]], sizeof(GeoRec));
+            std::memcpy(blob.data() + off_id + i * sizeof(int), &b.order[i], sizeof(int));
+        }
+        for (size_t i = 0; i < n_big; ++i) {
+            std::memcpy(blob.data() + off_bgeo + i * sizeof(GeoRec), &geo[b.big[i]], sizeof(GeoRec));
+            std::memcpy(blob.data() + off_bid + i * sizeof(int), &b.big[i], sizeof(int));
+        }
+        if (hipMalloc(&ctx->d_bvh, total) != hipSuccess) {
+            ptg_context_destroy(ctx);
+            return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the BVH failed");
+        }
+        PTG_HIP(hipMemcpy(ctx->d_bvh, blob.data(), total, hipMemcpyHostToDevice));
+        unsigned char *base = static_cast<unsigned char *>(ctx->d_bvh);
+        A.bvh_nodes = reinterpret_cast<const float4 *>(base);
+        A.bvh_geo = reinterpret_cast<const GeoRec *>(base + off_geo);
+        A.bvh_id = reinterpret_cast<const int *>(base + off_id);
+        A.big_geo = reinterpret_cast<const GeoRec *>(base + off_bgeo);
+        A.big_id = reinterpret_cast<const int *>(base + off_bid);
+        A.n_nodes = (int)n_nodes;
+        A.n_big = (int)n_big;
+    }
     A.pos_x = (float)cam->position[0];
     A.pos_y = (float)cam->position[1];
     A.pos_z = (float)cam->position[2];
@@ -829,6 +972,8 @@ int ptg_context_destroy(ptg_context *ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_shade);
+    if (ctx->d_bvh)
+        (void)hipFree(ctx->d_bvh);
     if (ctx->d_acc)
         (void)hipFree(ctx->d_acc);
     delete ctx;
@@ -862,11 +1007,11 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
 {
     if (grid <= 0)
         return PTG_OK;
-    const bool lds = A.n <= kMaxLdsSpheres;
+    const bool bvh = A.n > kLinearMax;
     if (count)
-        lds ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, 0, s>>>(A);
+        bvh ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, 0, s>>>(A);
     else
-        lds ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, 0, s>>>(A);
+        bvh ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, 0, s>>>(A);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }
@@ -984,7 +1129,10 @@ int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const i
     fill_launch(ctx, params, A, grid);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int blocks = (int)((n + kBlock - 1) / kBlock);
-    trace_kernel<<<blocks, kBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+    if (A.n > kLinearMax)
+        trace_kernel<true><<<blocks, kBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+    else
+        trace_kernel<false><<<blocks, kBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }

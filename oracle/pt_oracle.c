@@ -718,6 +718,66 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
     return id >= 0;
 }
 
+/* Scenes with more than LINEAR_MAX spheres (the GPU walks a BVH there): the
+ * reference's own rule -- every candidate root divided, t = fl(num/den), the
+ * smallest t wins, lowest index on ties (main.cpp:35 strict < in index order).
+ * Per-sphere arithmetic as intersect_B; the cull compares against tb. */
+#define LINEAR_MAX 64
+static int intersect_B_lex(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
+{
+    float a = fdot(d, d);
+    float tb = INFF;
+    int id = -1;
+    for (int i = 0; i < n; ++i) {
+        const sphB *sp = &s[i];
+        f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
+        float ed = fdot(e, d);
+        float ee = fdot(e, e);
+        float hb, c;
+        if (sp->big) {
+            hb = fmaf(sp->R, fdot(sp->N, d), ed);
+            c = fmaf(sp->R2x, fdot(e, sp->N), ee);
+        } else {
+            hb = ed;
+            c = ee + sp->negR2;
+        }
+        if (hb >= 0.0f && c >= 0.0f)
+            continue;
+        if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * CULL_MARGIN)
+            continue;
+        float disc = fmaf(hb, hb, -(a * c));
+        if (disc < 0.0f)
+            continue;
+        float sq = sqrt_B(disc);
+        float num, den;
+        if (hb < 0.0f) {
+            float q = sq - hb;
+            num = c;
+            den = q;
+            if (c < EPSF * q) {
+                num = q;
+                den = a;
+                if (q < EPSF * a)
+                    continue;
+            }
+        } else {
+            float qn = hb + sq;
+            num = -c;
+            den = qn;
+            if (num < EPSF * den)
+                continue;
+        }
+        float t = num / den;
+        if (t < tb) {
+            tb = t;
+            id = i;
+        }
+    }
+    *tout = tb;
+    *idout = id;
+    return id >= 0;
+}
+
 static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y, int sx, int sy,
                    uint32_t st, int *segs)
 {
@@ -747,7 +807,7 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y
         float t;
         int id;
         (*segs)++;
-        if (!intersect_B(s, n, o, d, &t, &id)) {
+        if (!(n > LINEAR_MAX ? intersect_B_lex(s, n, o, d, &t, &id) : intersect_B(s, n, o, d, &t, &id))) {
             f3 ud = fnorm(d);
             float tt = 0.5f * (ud.y + 1.0f);
             float it = 1.0f - tt;

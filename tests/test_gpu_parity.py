@@ -54,7 +54,9 @@ def _check_equal(gpu, ref):
     assert float(diff.max()) == 0.0, (float(diff.max()), int((diff > 0).sum()))
 
 
-CASES = [("box", 64, 48, 16), ("box_mirror", 64, 36, 16), ("simple", 80, 60, 16), ("synthetic:300", 64, 36, 8)]
+# > 64 spheres: BVH traversal on the GPU, linear scan with the same nearest-hit rule in the oracle
+CASES = [("box", 64, 48, 16), ("box_mirror", 64, 36, 16), ("simple", 80, 60, 16), ("synthetic:300", 64, 36, 8),
+         ("synthetic:10000", 48, 27, 4)]
 
 
 @pytest.mark.parametrize("name,W,H,samps", CASES)
@@ -69,7 +71,7 @@ def test_image_bitexact_vs_oracle(name, W, H, samps):
     assert gsegs == rsegs
 
 
-@pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300"])
+@pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:3000"])
 def test_per_path_radiance_bitexact(name):
     _require_gpu()
     W, H = 160, 120
