@@ -135,16 +135,18 @@ def main():
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     ctx = ptgpu.Context(scn, cam, device=local)
     params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk)
+    cparams = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
+                                flags=ptgpu.FLAG_COUNT_TESTS)
     rows = ptgpu.shard_rows(H, args.band_rows, world)
     slab = torch.zeros(rows * W * 3, dtype=torch.float32, device=dev)
     my_rows = int((ptgpu.slab_to_image_rows(H, args.band_rows, rank, world) >= 0).sum())
-    segs = torch.zeros(1, dtype=torch.int64, device=dev)
+    segs = torch.zeros(3, dtype=torch.int64, device=dev)  # scene scans, sphere tests, BVH box tests
     stream = torch.cuda.current_stream(dev)
 
     def step(count=False, events=None):
         if events is not None:
             events[0].record(stream)
-        ctx.render_device(slab, params, segs if count else None, stream)
+        ctx.render_device(slab, cparams if count else params, segs if count else None, stream)
         if events is not None:
             events[1].record(stream)
         if world > 1:
@@ -154,7 +156,7 @@ def main():
     # S_bar from the kernel's own segment counter (untimed)
     step(count=True)
     torch.cuda.synchronize()
-    seg_local = int(segs.item())
+    seg_local, sph_local, box_local = (int(v) for v in segs.cpu().tolist())
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
@@ -179,13 +181,18 @@ def main():
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
-        s = torch.tensor([seg_local], dtype=torch.int64, device=cdev)
+        s = torch.tensor([seg_local, sph_local, box_local], dtype=torch.int64, device=cdev)
         dist.all_reduce(s)
-        seg_total = int(s.item())
+        seg_total, sph_local, box_local = (int(v) for v in s.cpu().tolist())
     frame_samples = W * H * spp
     s_bar = seg_total / frame_samples
     n_sph = ctx.n_spheres
-    flop_per_sample = s_bar * (23 * n_sph + 100) + 60
+    # S_bar*(23*N + 100) + 60 per sample for the linear scan;
+    # generalised to the tests actually executed (BVH scenes): 23 FLOP per
+    # ray-sphere test, 12 per slab box test, 100 per segment, 60 per sample
+    tests_per_sample = sph_local / frame_samples
+    boxes_per_sample = box_local / frame_samples
+    flop_per_sample = 23 * tests_per_sample + 12 * boxes_per_sample + 100 * s_bar + 60
     my_samples = my_rows * W * spp
     achieved = my_samples * flop_per_sample / (kern_ms / 1e3) / 1e12 if kern_ms > 0 else None
 
@@ -220,7 +227,10 @@ def main():
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
                          "traffic": traffic,
                          "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
-                         "segments_per_sample": round(s_bar, 4)},
+                         "segments_per_sample": round(s_bar, 4),
+                         "sphere_tests_per_segment": round(tests_per_sample / s_bar, 2) if s_bar else None,
+                         "box_tests_per_segment": round(boxes_per_sample / s_bar, 2) if s_bar else None,
+                         "scan": "bvh" if n_sph > 64 else "linear"},
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -96,6 +96,7 @@ struct KArgs {
     int chunk, n_groups, single_chunk;
     int sample_begin, sample_end;  // samples [begin, end) of every sub-pixel in this launch
     int keep_acc;                  // resolve without re-zeroing (progressive previews)
+    int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
     long long n_units;
     float *out;
     unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
@@ -221,6 +222,10 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
 // ties (main.cpp:35 strict <, in index order) -- which does not depend on the
 // visiting order, so the oracle reproduces it with a linear scan.  Box tests
 // only cull: boxes are padded (bvh_build.hpp) and use fast reciprocals.
+struct ScanCount {
+    uint32_t spheres = 0, boxes = 0;  // sphere tests and box tests of the BVH walk (counting kernel only)
+};
+
 __device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1, const int gid, const f3 o,
                                                 const f3 d, const float a, float &tb, int &id)
 {
@@ -268,13 +273,16 @@ __device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1
     }
 }
 
-__device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest)
+template <bool kCount>
+__device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest, ScanCount &cnt)
 {
     const float a = dot3(d, d);
     float tb = kInf;
     int id = -1;
     for (int k = 0; k < A.n_big; ++k)
         test_sphere_lex(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tb, id);
+    if constexpr (kCount)
+        cnt.spheres += A.n_big;
     // slab test (culling only: fast reciprocals, padded boxes)
     const float ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
     const float iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
@@ -284,6 +292,8 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     while (ni < A.n_nodes) {
         const float4 n0 = A.bvh_nodes[2 * ni];
         const float4 n1 = A.bvh_nodes[2 * ni + 1];
+        if constexpr (kCount)
+            cnt.boxes += 1;
         float tx1 = __builtin_fmaf(n0.x, ix, -ox), tx2 = __builtin_fmaf(n1.x, ix, -ox);
         float ty1 = __builtin_fmaf(n0.y, iy, -oy), ty2 = __builtin_fmaf(n1.y, iy, -oy);
         float tz1 = __builtin_fmaf(n0.z, iz, -oz), tz2 = __builtin_fmaf(n1.z, iz, -oz);
@@ -297,8 +307,10 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
         }
         const int leaf = __float_as_int(n1.w);
         if (leaf >= 0) {
-            const int first = leaf & 0xFFFFFF, cnt = leaf >> 24;
-            for (int j = 0; j < cnt; ++j)
+            const int first = leaf & 0xFFFFFF, nl = leaf >> 24;
+            if constexpr (kCount)
+                cnt.spheres += nl;
+            for (int j = 0; j < nl; ++j)
                 test_sphere_lex(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d, a, tb,
                                 id);
         }
@@ -311,12 +323,16 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
-template <bool kBvh>
+template <bool kBvh, bool kCount = false>
 __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const ShadeRec *shade, f3 &o, f3 &d, f3 &T,
-                                        f3 &E, int &depth, uint32_t &st)
+                                        f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
 {
     float t;
-    int id = kBvh ? scene_scan_bvh(A, o, d, t) : scene_scan(A, geo, o, d, t);
+    int id;
+    if constexpr (kBvh)
+        id = scene_scan_bvh<kCount>(A, o, d, t, cnt);
+    else
+        id = scene_scan(A, geo, o, d, t);
     if (id < 0) {  // main.cpp:115-120: sky
         f3 ud = norm3(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -506,7 +522,8 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     f3 o, d, T, E;
     int depth = 0;
     uint32_t st = 0;
-    uint32_t segs = 0;
+    uint32_t segs = 0;  // scene scans executed by this lane
+    ScanCount scnt;     // BVH sphere/box tests (counting kernel)
     auto start = [&](int it) {
         int sample;
         if (nv == 64) {  // full pixel group (the common case): shifts
@@ -543,7 +560,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            if (segment<kBvh>(A, geo, shade, o, d, T, E, depth, st)) {
+            if (segment<kBvh, kCount>(A, geo, shade, o, d, T, E, depth, st, scnt)) {
                 atomicAdd(&lds_acc[wv][slot], quant(E.x));
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
                 atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
@@ -566,11 +583,18 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         }
     }
     if constexpr (kCount) {
-        unsigned long long ws = segs;
-        for (int off = 32; off > 0; off >>= 1)
+        unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes;
+        for (int off = 32; off > 0; off >>= 1) {
             ws += __shfl_xor(ws, off, 64);
+            wsph += __shfl_xor(wsph, off, 64);
+            wbox += __shfl_xor(wbox, off, 64);
+        }
         if (lane == 0 && ws)
             atomicAdd(A.segments, ws);
+        if (lane == 0 && A.count_tests) {
+            atomicAdd(A.segments + 1, kBvh ? wsph : ws * (unsigned long long)A.n);
+            atomicAdd(A.segments + 2, wbox);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -661,7 +685,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     bool done = false;
     while (!done) {
         segs += 1;
-        done = segment<kBvh>(A, A.geo, A.shade, o, d, T, E, depth, st);
+        ScanCount scnt;
+        done = segment<kBvh>(A, A.geo, A.shade, o, d, T, E, depth, st, scnt);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -818,6 +843,7 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     A.sample_begin = s_begin;
     A.sample_end = s_end;
     A.keep_acc = 0;
+    A.count_tests = (p->flags & PTG_FLAG_COUNT_TESTS) != 0;
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.

@@ -44,10 +44,13 @@ def _camera_array(cam) -> np.ndarray:
     return a
 
 
+FLAG_COUNT_TESTS = 1  # include/ptgpu.h PTG_FLAG_COUNT_TESTS
+
+
 def make_params(width, height, samples, num_subpixels=2, seed=DEFAULT_SEED, band_rows=DEFAULT_BAND_ROWS,
-                shard_rank=0, shard_count=1, chunk_samples=0) -> Params:
+                shard_rank=0, shard_count=1, chunk_samples=0, flags=0) -> Params:
     return Params(int(width), int(height), int(samples), int(num_subpixels), int(seed) & (2**64 - 1),
-                  int(band_rows), int(shard_rank), int(shard_count), int(chunk_samples), 0)
+                  int(band_rows), int(shard_rank), int(shard_count), int(chunk_samples), int(flags))
 
 
 def shard_rows(height: int, band_rows: int, shard_count: int) -> int:
@@ -130,7 +133,7 @@ class Context:
         _check_tensor(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
                       * params.width * 3)
         if segments is not None:
-            _check_tensor(segments, torch.int64, 1)
+            _check_tensor(segments, torch.int64, 3 if params.flags & FLAG_COUNT_TESTS else 1)
         s = (stream or torch.cuda.current_stream(out.device)).cuda_stream
         check(lib().ptg_render_device(self._h, C.byref(params), C.c_void_p(out.data_ptr()),
                                       C.c_void_p(segments.data_ptr()) if segments is not None else None,

@@ -82,8 +82,13 @@ typedef struct ptg_params {
     int32_t shard_rank;     /* this shard renders bands b with b % shard_count == shard_rank */
     int32_t shard_count;    /* 1 = whole image */
     int32_t chunk_samples;  /* samples per sub-pixel per work unit (0 = auto); results do not depend on it */
-    int32_t flags;          /* reserved, 0 */
+    int32_t flags;          /* PTG_FLAG_* */
 } ptg_params;
+
+/* flags: with PTG_FLAG_COUNT_TESTS, d_segments of ptg_render_device /
+ * ptg_accumulate_device points to 3 counters: += scene scans, sphere tests
+ * (ray-sphere quadratics), BVH box tests -- the inputs of the roofline model. */
+#define PTG_FLAG_COUNT_TESTS 1
 
 typedef struct ptg_context ptg_context;
 

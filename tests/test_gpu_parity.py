@@ -34,17 +34,20 @@ def _oracle_scene(scn, cam):
 
 def _gpu_image(scn, cam, W, H, samps, nsub=2, seed=SEED, band_rows=8, rank=0, count=1, count_segments=False,
                chunk=0):
-    p = ptgpu.make_params(W, H, samps, nsub, seed, band_rows, rank, count, chunk)
+    p = ptgpu.make_params(W, H, samps, nsub, seed, band_rows, rank, count, chunk,
+                          flags=ptgpu.FLAG_COUNT_TESTS if count_segments else 0)
     rows = ptgpu.shard_rows(H, band_rows, count)
     out = torch.full((rows * W * 3,), -7.0, dtype=torch.float32, device="cuda")
-    segs = torch.zeros(1, dtype=torch.int64, device="cuda") if count_segments else None
+    segs = torch.zeros(3, dtype=torch.int64, device="cuda") if count_segments else None
     with ptgpu.Context(scn, cam) as ctx:
         ctx.render_device(out, p, segs)
         torch.cuda.synchronize()
     img = out.cpu().numpy().reshape(rows, W, 3)
     if count == 1:
         img = img[:H]
-    return img, (int(segs.item()) if segs is not None else None)
+    if segs is not None:
+        _gpu_image.tests = segs.cpu().tolist()
+    return img, (int(segs[0].item()) if segs is not None else None)
 
 
 def _check_equal(gpu, ref):
@@ -69,6 +72,12 @@ def test_image_bitexact_vs_oracle(name, W, H, samps):
     ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
     _check_equal(gpu, ref)
     assert gsegs == rsegs
+    nseg, ntest, nbox = _gpu_image.tests
+    n = len(scn.spheres)
+    if n <= 64:  # linear scan: every sphere per segment, no boxes
+        assert ntest == nseg * n and nbox == 0
+    else:  # BVH: far fewer sphere tests than the linear scan
+        assert 0 < ntest < nseg * n / 5 and nbox > 0
 
 
 @pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:3000"])
