@@ -67,14 +67,7 @@ __device__ __forceinline__ uint64_t key_hash(uint64_t seed, uint64_t pixel_sub)
 }
 __device__ __forceinline__ uint32_t sample_state(uint64_t key, uint32_t sample)
 {
-#ifdef PTG_HASH32  // speed probe only (not the oracle's definition)
-    uint32_t h = (uint32_t)key ^ (uint32_t)(key >> 32) ^ ((sample + 1u) * 0x9E3779B9u);
-    h = (h ^ (h >> 16)) * 0x85EBCA6Bu;
-    h = (h ^ (h >> 13)) * 0xC2B2AE35u;
-    uint32_t st = h ^ (h >> 16);
-#else
     uint32_t st = (uint32_t)(mix64(key + ((uint64_t)sample + 1ull) * 0x9E3779B97F4A7C15ull) >> 32);
-#endif
     return st ? st : 0x6D2B79F5u;
 }
 // one U[0,1) draw: xorshift32 (13,17,5), top 24 bits

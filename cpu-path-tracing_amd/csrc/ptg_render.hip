@@ -53,21 +53,21 @@ constexpr int kBlock = 256;        // 4 waves per workgroup
 #ifndef PTG_MAX_LDS_SPHERES
 #define PTG_MAX_LDS_SPHERES 64
 #endif
-// scenes up to 64 spheres keep geometry (2 KB) and shading records (4 KB) in
-// LDS: 15 KB per workgroup, 8 workgroups per CU (measured: +1.3 % over
-// geometry-only staging of up to 256 spheres, which itself beat scalar loads)
+// scenes up to 64 spheres keep geometry (32 B) and shading (64 B) records in
+// dynamically sized LDS: box_scene needs 17.4 KB + 768 B per workgroup, so 8
+// workgroups fit a CU (measured: shading in LDS +1.3 % over geometry-only
+// staging, which itself beat scalar loads by 1.5 %)
 constexpr int kMaxLdsSpheres = PTG_MAX_LDS_SPHERES;
 // nearest-hit rule and scan: <= kLinearMax spheres -> linear scan from LDS with
 // fraction comparisons; more -> BVH with the reference's per-candidate
 // division rule (DESIGN.md "scene scan"); the oracle switches at the same n
-constexpr int kLinearMax = 64;
-static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
-#ifndef PTG_SCAN_BRANCHES  // measured: the branchless scan is 1.4 % faster (fewer exec-mask SALU ops)
-#define PTG_SCAN_BRANCHLESS 1
+#ifndef PTG_LINEAR_MAX
+#define PTG_LINEAR_MAX 64
 #endif
-#define PTG_UNIFORM_BIG 1
-#ifndef PTG_RESTART_BATCH
-#define PTG_RESTART_BATCH 8  // measured: 8 beats 1, 4, 16 (profiles/)
+constexpr int kLinearMax = PTG_LINEAR_MAX;
+static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
+#ifndef PTG_REFILL_BATCH
+#define PTG_REFILL_BATCH 32  // measured: 32 beats 16 and ties 48 (DESIGN.md perf log)
 #endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
@@ -166,11 +166,7 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
         float ed = dot3(e, d);
         float ee = dot3(e, e);
         float hb, c;
-#ifdef PTG_UNIFORM_BIG
         const bool big = __builtin_amdgcn_readfirstlane(__float_as_int(g0.w)) >= 0;  // same record in every lane
-#else
-        const bool big = g0.w >= 0.0f;
-#endif
         if (big) {  // huge sphere: anchored form
             hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
@@ -178,8 +174,8 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             hb = ed;
             c = ee + g1.w;
         }
-#ifdef PTG_SCAN_BRANCHLESS
-        // same arithmetic as below, decided by selects instead of branches
+        // culls, eps tests and the comparison decided by selects, not branches
+        // (fewer exec-mask SALU instructions; measured 1.4 % faster)
         const bool skip = (hb >= 0.0f && c >= 0.0f) || (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * kCullMargin);
         const float disc = __builtin_fmaf(hb, hb, -(a * c));
         const float sq = sqrt_d(disc);
@@ -194,39 +190,6 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             bq = den;
             id = i;
         }
-#else
-        if (hb >= 0.0f && c >= 0.0f)
-            continue;
-        if (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * kCullMargin)
-            continue;
-        float disc = __builtin_fmaf(hb, hb, -(a * c));
-        if (disc < 0.0f)
-            continue;
-        float sq = sqrt_d(disc);
-        float num, den;
-        if (hb < 0.0f) {
-            float q = sq - hb;  // > 0; roots c/q (near) and q/a (far)
-            num = c;
-            den = q;
-            if (c < kEps * q) {  // near root < eps
-                num = q;
-                den = a;
-                if (q < kEps * a)
-                    continue;
-            }
-        } else {
-            float qn = hb + sq;  // > 0 here (c < 0): root c/-qn
-            num = -c;
-            den = qn;
-            if (num < kEps * den)
-                continue;
-        }
-        if (num * bq < bn * den) {
-            bn = num;
-            bq = den;
-            id = i;
-        }
-#endif
     }
     tbest = id >= 0 ? bn / bq : kInf;
     return id;
@@ -243,6 +206,7 @@ struct ScanCount {
     uint32_t spheres = 0, boxes = 0;  // sphere tests and box tests of the BVH walk (counting kernel only)
 };
 
+template <bool kMaybeBig>  // BVH leaves hold only non-huge spheres (bvh_build.hpp)
 __device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1, const int gid, const f3 o,
                                                 const f3 d, const float a, float &tb, int &id)
 {
@@ -250,7 +214,7 @@ __device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1
     float ed = dot3(e, d);
     float ee = dot3(e, e);
     float hb, c;
-    if (g0.w >= 0.0f) {
+    if (kMaybeBig && g0.w >= 0.0f) {
         hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
         c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
     } else {
@@ -297,7 +261,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     float tb = kInf;
     int id = -1;
     for (int k = 0; k < A.n_big; ++k)
-        test_sphere_lex(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tb, id);
+        test_sphere_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tb, id);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
     // slab test (culling only: fast reciprocals, padded boxes)
@@ -328,8 +292,8 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
             if constexpr (kCount)
                 cnt.spheres += nl;
             for (int j = 0; j < nl; ++j)
-                test_sphere_lex(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d, a, tb,
-                                id);
+                test_sphere_lex<false>(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d,
+                                       a, tb, id);
         }
         ++ni;
     }
@@ -484,10 +448,13 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     // ds_read_b128 broadcasts in the scan, by-id gathers at hits); larger
     // scenes read geometry with wave-uniform scalar loads from L2/HBM instead
     constexpr bool kLdsGeo = !kBvh;  // linear scenes (<= kMaxLdsSpheres) live in LDS
-    __shared__ GeoRec lds_geo[kLdsGeo ? kMaxLdsSpheres : 1];
+    // dynamic LDS: n geometry records then n shading records (96 B/sphere),
+    // sized at launch so small scenes keep 8 workgroups per CU
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+    GeoRec *lds_geo = reinterpret_cast<GeoRec *>(dyn_lds);
+    ShadeRec *lds_shade = reinterpret_cast<ShadeRec *>(dyn_lds + (size_t)A.n * sizeof(GeoRec));
     const GeoRec *geo = A.geo;
     const ShadeRec *shade = A.shade;
-    __shared__ ShadeRec lds_shade[kLdsGeo ? kMaxLdsSpheres : 1];
     if constexpr (kLdsGeo) {
         for (int i = threadIdx.x; i < A.n; i += kBlock) {
             lds_geo[i] = A.geo[i];
@@ -541,36 +508,59 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     uint32_t st = 0;
     uint32_t segs = 0;  // scene scans executed by this lane
     ScanCount scnt;     // BVH sphere/box tests (counting kernel)
-    auto start = [&](int it) {
-        int sample;
-        if (nv == 64) {  // full pixel group (the common case): shifts
-            slot = it & 63;
+    // Each lane keeps its NEXT path's camera ray prefetched in LDS: a lane
+    // whose path ends starts the prefetched one at once (two LDS reads), and
+    // the camera code runs only in refills of >= PTG_REFILL_BATCH lanes (or
+    // when a lane would otherwise idle).
+    __shared__ float4 lds_pre[kWavesPerBlock][64][2];
+    auto ray_of = [&](int it, f3 &ro, f3 &rd, uint32_t &rs) {
+        int sl, sample;
+        if (nv == 64) {
+            sl = it & 63;
             sample = s0 + (it >> 6);
         } else {
-            slot = it % nv;
+            sl = it % nv;
             sample = s0 + it / nv;
         }
         Lane L;
-        uint32_t pk = lds_pix[wv][slot];
+        uint32_t pk = lds_pix[wv][sl];
         L.x = (int)(pk & 0xFFFFFu);
         L.y = y;
         L.sx = (int)((pk >> 20) & 63u);
         L.sy = (int)(pk >> 26);
-        L.key = lds_key[wv][slot];
-        camera_ray(A, L, (uint32_t)sample, st, o, d);
+        L.key = lds_key[wv][sl];
+        camera_ray(A, L, (uint32_t)sample, rs, ro, rd);
+    };
+    auto begin = [&](int it, f3 ro, f3 rd, uint32_t rs) {
+        item = it;
+        slot = nv == 64 ? (it & 63) : it % nv;
+        o = ro;
+        d = rd;
+        st = rs;
         T = mk3(1.0f, 1.0f, 1.0f);
         E = mk3(0.0f, 0.0f, 0.0f);
         depth = 0;
     };
-    if (item >= 0)
-        start(item);
-    int next = total < 64 ? total : 64;  // wave-uniform pool cursor
-    // flat loop: one iteration = one bounce segment for every live lane
-    // flat loop: one iteration = one bounce segment for every live lane.  A
-    // finished lane waits until PTG_RESTART_BATCH lanes are waiting (or none
-    // is live, or the pool is empty), then the waiting lanes take the next
-    // unstarted paths together -- fewer, fuller executions of the restart code.
-    bool waiting = false;
+    auto store_pre = [&](int it, f3 ro, f3 rd, uint32_t rs) {
+        lds_pre[wv][lane][0] = make_float4(ro.x, ro.y, rd.x, rd.y);
+        lds_pre[wv][lane][1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), 0.0f);
+    };
+    if (item >= 0) {
+        f3 ro, rd;
+        uint32_t rs;
+        ray_of(item, ro, rd, rs);
+        begin(item, ro, rd, rs);
+    }
+    bool has_pre = false;
+    if (64 + lane < total) {
+        f3 ro, rd;
+        uint32_t rs;
+        ray_of(64 + lane, ro, rd, rs);
+        store_pre(64 + lane, ro, rd, rs);
+        has_pre = true;
+    }
+    int next = total < 128 ? total : 128;  // wave-uniform pool cursor
+    bool waiting = false;                  // path ended, no prefetched ray yet
     for (;;) {
         if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
             break;
@@ -582,21 +572,39 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                 atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
                 atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
                 item = -1;
-                waiting = true;
+                if (has_pre) {
+                    const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
+                    begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x),
+                          __float_as_uint(p1.y));
+                    has_pre = false;
+                } else {
+                    waiting = true;
+                }
             }
         }
-        const unsigned long long wm = __ballot(waiting);
-        const int nw = (int)__popcll(wm);
-        if (nw > 0 && (nw >= PTG_RESTART_BATCH || __ballot(item >= 0) == 0ull || next >= total)) {
-            if (waiting) {
-                int ni = next + (int)__popcll(wm & ((1ull << lane) - 1ull));
-                if (ni < total) {
-                    item = ni;
-                    start(item);
+        if (next < total) {
+            const unsigned long long need = __ballot(!has_pre);
+            const int nn = (int)__popcll(need);
+            if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
+                if (!has_pre) {
+                    const int ni = next + (int)__popcll(need & ((1ull << lane) - 1ull));
+                    if (ni < total) {
+                        f3 ro, rd;
+                        uint32_t rs;
+                        ray_of(ni, ro, rd, rs);
+                        if (waiting || item < 0) {  // idle lane: start it now
+                            begin(ni, ro, rd, rs);
+                            waiting = false;
+                        } else {
+                            store_pre(ni, ro, rd, rs);
+                            has_pre = true;
+                        }
+                    }
                 }
-                waiting = false;
+                next += nn;
             }
-            next += nw;
+        } else {
+            waiting = false;  // pool exhausted: nothing left for this lane
         }
     }
     if constexpr (kCount) {
@@ -1051,10 +1059,11 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     if (grid <= 0)
         return PTG_OK;
     const bool bvh = A.n > kLinearMax;
+    const size_t lds = bvh ? 0 : (size_t)A.n * (sizeof(GeoRec) + sizeof(ShadeRec));
     if (count)
-        bvh ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, 0, s>>>(A);
+        bvh ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, lds, s>>>(A);
     else
-        bvh ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, 0, s>>>(A);
+        bvh ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, lds, s>>>(A);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }
