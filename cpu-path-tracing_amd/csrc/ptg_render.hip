@@ -140,17 +140,17 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 }
 
 // main.cpp:30-42 + sphere.cpp:6-30: closest root >= eps over all spheres,
-// strict < so the lowest index wins ties.  Sphere records are loaded with
-// wave-uniform addresses -> scalar loads (SGPR operands, no VGPR/LDS traffic).
-// Roots: with q = -(hb + sign(hb) sqrt(disc)) they are c/q and q/a; c/q is
-// the nearer one whenever hb < 0, the far root q/a matters only when the near
-// one is < eps.  Roots stay fractions num/den (den > 0): "root < eps" is
-// num < eps*den, "nearer" is num*bq < bn*den, and one division per segment
-// turns the winner into t.  Two culls skip spheres that cannot win without
-// the sqrt (DESIGN.md "scene scan"):
-//   hb >= 0 && c >= 0                             both roots <= 0
-//   hb < 0 && c > 0 && c*bq >= bn*2|hb|*(1+2^-20)  near root not nearer (q <= 2|hb|(1+3u))
-constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20
+// strict < so the lowest index wins ties.  Sphere records are read from LDS
+// at wave-uniform addresses (broadcast reads).
+// Roots: with qq = sq + |hb| they are c/-qq (hb >= 0) or c/qq (near) and
+// qq/a (far) (hb < 0); the far root matters only when the near one is < eps.
+// Roots stay fractions num/den (den > 0): "root < eps" is num < eps*den,
+// "nearer" is num*bq < bn*den, and one division per segment turns the winner
+// into t.  The test is straight-line code (selects, no per-lane branches):
+// the oracle's two culls (hb >= 0 && c >= 0; near root provably not nearer,
+// DESIGN.md "scene scan") are exact early-outs that never let a wave skip the
+// sqrt in practice, so they are left out here (-15 % frame time, same bits).
+constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test, PTG_SCAN_CULL)
 
 __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
 {
@@ -159,7 +159,7 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     int id = -1;
-    for (int i = 0; i < A.n; ++i) {
+    auto test = [&](const int i) {
         float4 g0 = geo[i].g0;
         float4 g1 = geo[i].g1;
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
@@ -174,23 +174,28 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             hb = ed;
             c = ee + g1.w;
         }
-        // culls, eps tests and the comparison decided by selects, not branches
-        // (fewer exec-mask SALU instructions; measured 1.4 % faster)
+#if defined(PTG_SCAN_CULL)
         const bool skip = (hb >= 0.0f && c >= 0.0f) || (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * kCullMargin);
+#else
+        const bool skip = false;
+#endif
         const float disc = __builtin_fmaf(hb, hb, -(a * c));
         const float sq = sqrt_d(disc);
         const bool neg = hb < 0.0f;
-        const float q = sq - hb, qn = hb + sq;
-        const bool near_lt = c < kEps * q;
-        const float num = neg ? (near_lt ? q : c) : -c;
-        const float den = neg ? (near_lt ? a : q) : qn;
-        const bool rej = neg ? (near_lt && q < kEps * a) : (-c < kEps * qn);
-        if (!skip && !(disc < 0.0f) && !rej && num * bq < bn * den) {
-            bn = num;
-            bq = den;
-            id = i;
-        }
-    }
+        // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
+        const float qq = sq + __builtin_fabsf(hb);
+        const bool near_lt = c < kEps * qq;
+        const float num = neg ? (near_lt ? qq : c) : -c;
+        const float den = (neg & near_lt) ? a : qq;
+        // one eps test covers all three cases (for the near root it repeats
+        // near_lt, which is false there)
+        const bool win = !skip & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
+        bn = win ? num : bn;
+        bq = win ? den : bq;
+        id = win ? i : id;
+    };
+    for (int i = 0; i < A.n; ++i)
+        test(i);
     tbest = id >= 0 ? bn / bq : kInf;
     return id;
 }
