@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/ptgpu.h"
@@ -79,6 +80,8 @@ struct KArgs {
     const GeoRec *geo;
     const ShadeRec *shade;
     int n;
+    int n_big_prefix;  // spheres [0, n_big_prefix) are huge (anchored form), and
+    int big_after;     // whether any sphere after the prefix is huge as well
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
     const GeoRec *bvh_geo;    // leaf-ordered geometry
@@ -150,7 +153,9 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 // the oracle's two culls (hb >= 0 && c >= 0; near root provably not nearer,
 // DESIGN.md "scene scan") are exact early-outs that never let a wave skip the
 // sqrt in practice, so they are left out here (-15 % frame time, same bits).
-constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test, PTG_SCAN_CULL)
+constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
+
+enum : int { kSmall = 0, kBig = 1, kEither = 2 };
 
 __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
 {
@@ -159,14 +164,17 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     int id = -1;
-    auto test = [&](const int i) {
+    auto test = [&](const int i, auto kind_tag) {
+        constexpr int kKind = decltype(kind_tag)::value;
         float4 g0 = geo[i].g0;
         float4 g1 = geo[i].g1;
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
         float ed = dot3(e, d);
         float ee = dot3(e, e);
         float hb, c;
-        const bool big = __builtin_amdgcn_readfirstlane(__float_as_int(g0.w)) >= 0;  // same record in every lane
+        bool big = kKind == kBig;
+        if constexpr (kKind == kEither)
+            big = __builtin_amdgcn_readfirstlane(__float_as_int(g0.w)) >= 0;  // same record in every lane
         if (big) {  // huge sphere: anchored form
             hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
@@ -174,13 +182,15 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             hb = ed;
             c = ee + g1.w;
         }
-#if defined(PTG_SCAN_CULL)
-        const bool skip = (hb >= 0.0f && c >= 0.0f) || (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * kCullMargin);
-#else
-        const bool skip = false;
-#endif
         const float disc = __builtin_fmaf(hb, hb, -(a * c));
-        const float sq = sqrt_d(disc);
+        float sq;
+        if constexpr (kKind == kBig) {
+            // walls are hit by most lanes: no branch around the sqrt
+            const float r = disc * rsqrt_d(disc);
+            sq = disc > 0.0f ? r : 0.0f;
+        } else {
+            sq = sqrt_d(disc);  // a wave whose lanes all miss skips it
+        }
         const bool neg = hb < 0.0f;
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
@@ -189,13 +199,23 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
         const float den = (neg & near_lt) ? a : qq;
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
-        const bool win = !skip & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
+        const bool win = !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
         bn = win ? num : bn;
         bq = win ? den : bq;
         id = win ? i : id;
     };
-    for (int i = 0; i < A.n; ++i)
-        test(i);
+    // index order is kept (ties go to the lowest index): huge-sphere prefix,
+    // then the rest
+    int i = 0;
+    for (; i < A.n_big_prefix; ++i)
+        test(i, std::integral_constant<int, kBig>{});
+    if (A.big_after) {
+        for (; i < A.n; ++i)
+            test(i, std::integral_constant<int, kEither>{});
+    } else {
+        for (; i < A.n; ++i)
+            test(i, std::integral_constant<int, kSmall>{});
+    }
     tbest = id >= 0 ? bn / bq : kInf;
     return id;
 }
@@ -972,6 +992,10 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.geo = ctx->d_geo;
     A.shade = ctx->d_shade;
     A.n = (int)n_spheres;
+    while (A.n_big_prefix < A.n && spheres[A.n_big_prefix].radius >= kBigRadius)
+        ++A.n_big_prefix;
+    for (int i = A.n_big_prefix; i < A.n; ++i)
+        A.big_after |= spheres[i].radius >= kBigRadius ? 1 : 0;
     if ((int)n_spheres > kLinearMax) {
         BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);
         const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();

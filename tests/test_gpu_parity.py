@@ -80,6 +80,23 @@ def test_image_bitexact_vs_oracle(name, W, H, samps):
         assert 0 < ntest < nseg * n / 5 and nbox > 0
 
 
+@pytest.mark.parametrize("order", [[5, 6, 7, 0, 1, 2, 3, 4], [0, 5, 1, 6, 2, 7, 3, 4], [7, 6, 5, 4, 3, 2, 1, 0]])
+def test_sphere_order_layouts(order):
+    """The scan runs the leading huge spheres (walls) in their own loop; scenes
+    whose huge spheres come after small ones take the per-record checked loop.
+    Every layout must stay bit-exact (same nearest-hit rule, same tie order)."""
+    _require_gpu()
+    W, H, samps = 48, 32, 8
+    scn = ptgpu.make_scene("box_mirror", W, H)
+    scn.spheres = [scn.spheres[i] for i in order]
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    gpu, gsegs = _gpu_image(scn, cam, W, H, samps, count_segments=True)
+    sp, ca = _oracle_scene(scn, cam)
+    ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
+    _check_equal(gpu, ref)
+    assert gsegs == rsegs
+
+
 @pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:3000"])
 def test_per_path_radiance_bitexact(name):
     _require_gpu()
