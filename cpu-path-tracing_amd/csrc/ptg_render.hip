@@ -586,6 +586,18 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     }
     int next = total < 128 ? total : 128;  // wave-uniform pool cursor
     bool waiting = false;                  // path ended, no prefetched ray yet
+    auto flush = [&](float ex, float ey, float ez, int sl) {
+        atomicAdd(&lds_acc[wv][sl], quant(ex));
+        atomicAdd(&lds_acc[wv][sl + 64], quant(ey));
+        atomicAdd(&lds_acc[wv][sl + 128], quant(ez));
+    };
+    // A finished path parks its radiance in registers (pe, pslot); the
+    // quantise + LDS adds run for all parked lanes at the next refill batch,
+    // not in every iteration in which some lane finishes.  A lane parks at
+    // most one path: it finishes a second one only after using its prefetched
+    // ray, and then it waits, which forces a batch.
+    float pe_x = 0.0f, pe_y = 0.0f, pe_z = 0.0f;
+    int pslot = -1;
     for (;;) {
         if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
             break;
@@ -593,17 +605,18 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
             if constexpr (kCount)
                 segs += 1;
             if (segment<kBvh, kCount>(A, geo, shade, o, d, T, E, depth, st, scnt)) {
-                atomicAdd(&lds_acc[wv][slot], quant(E.x));
-                atomicAdd(&lds_acc[wv][slot + 64], quant(E.y));
-                atomicAdd(&lds_acc[wv][slot + 128], quant(E.z));
                 item = -1;
                 if (has_pre) {
+                    pe_x = E.x;
+                    pe_y = E.y;
+                    pe_z = E.z;
+                    pslot = slot;
                     const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
                     begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x),
                           __float_as_uint(p1.y));
                     has_pre = false;
                 } else {
-                    waiting = true;
+                    waiting = true;  // E is kept until the batch
                 }
             }
         }
@@ -611,15 +624,25 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
             const unsigned long long need = __ballot(!has_pre);
             const int nn = (int)__popcll(need);
             if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
+                const bool idle = waiting || item < 0;
+                if (pslot >= 0)
+                    flush(pe_x, pe_y, pe_z, pslot);
+                pslot = -1;
+                if (waiting) {
+                    pe_x = E.x;
+                    pe_y = E.y;
+                    pe_z = E.z;
+                    pslot = slot;
+                }
+                waiting = false;
                 if (!has_pre) {
                     const int ni = next + (int)__popcll(need & ((1ull << lane) - 1ull));
                     if (ni < total) {
                         f3 ro, rd;
                         uint32_t rs;
                         ray_of(ni, ro, rd, rs);
-                        if (waiting || item < 0) {  // idle lane: start it now
+                        if (idle) {  // idle lane: start it now
                             begin(ni, ro, rd, rs);
-                            waiting = false;
                         } else {
                             store_pre(ni, ro, rd, rs);
                             has_pre = true;
@@ -628,10 +651,13 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                 }
                 next += nn;
             }
-        } else {
-            waiting = false;  // pool exhausted: nothing left for this lane
+        } else if (waiting) {  // pool exhausted: nothing left for this lane
+            flush(E.x, E.y, E.z, slot);
+            waiting = false;
         }
     }
+    if (pslot >= 0)
+        flush(pe_x, pe_y, pe_z, pslot);
     if constexpr (kCount) {
         unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes;
         for (int off = 32; off > 0; off >>= 1) {
