@@ -80,8 +80,12 @@ struct KArgs {
     const GeoRec *geo;
     const ShadeRec *shade;
     int n;
-    int n_big_prefix;  // spheres [0, n_big_prefix) are huge (anchored form), and
-    int big_after;     // whether any sphere after the prefix is huge as well
+    // linear scenes: records in SCAN order (prepare_scan_order), grouped by
+    // kind: [0, end_ax[0]) huge spheres anchored on the x axis, then y, then z
+    // ([end_ax[k-1], end_ax[k])), then general huge spheres up to end_big,
+    // then the small spheres up to n
+    int end_ax[3];
+    int end_big;
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
     const GeoRec *bvh_geo;    // leaf-ordered geometry
@@ -143,8 +147,13 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 }
 
 // main.cpp:30-42 + sphere.cpp:6-30: closest root >= eps over all spheres,
-// strict < so the lowest index wins ties.  Sphere records are read from LDS
-// at wave-uniform addresses (broadcast reads).
+// strict < so the first record in scan order wins exact ties.  Sphere records
+// are read from LDS at wave-uniform addresses (broadcast reads).
+// Scan order groups the records by kind (host: prepare_scan_order), so every
+// loop below runs one straight-line test: huge spheres whose anchor normal is
+// a coordinate axis (the box walls) need e_k and d_k instead of two dot
+// products (-6 VALU per wall); the oracle's generic form gives the same bits
+// (a dot product with +-e_k is exactly +-x_k).
 // Roots: with qq = sq + |hb| they are c/-qq (hb >= 0) or c/qq (near) and
 // qq/a (far) (hb < 0); the far root matters only when the near one is < eps.
 // Roots stay fractions num/den (den > 0): "root < eps" is num < eps*den,
@@ -155,7 +164,9 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 // sqrt in practice, so they are left out here (-15 % frame time, same bits).
 constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
 
-enum : int { kSmall = 0, kBig = 1, kEither = 2 };
+enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4 };
+
+__device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
 __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
 {
@@ -172,10 +183,10 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
         float ed = dot3(e, d);
         float ee = dot3(e, e);
         float hb, c;
-        bool big = kKind == kBig;
-        if constexpr (kKind == kEither)
-            big = __builtin_amdgcn_readfirstlane(__float_as_int(g0.w)) >= 0;  // same record in every lane
-        if (big) {  // huge sphere: anchored form
+        if constexpr (kKind <= kAxZ) {  // huge sphere anchored on axis k: g0.w = +-R, g1.w = +-2R
+            hb = __builtin_fmaf(g0.w, comp(d, kKind), ed);
+            c = __builtin_fmaf(g1.w, comp(e, kKind), ee);
+        } else if constexpr (kKind == kBig) {  // general anchored form
             hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
         } else {
@@ -183,14 +194,10 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             c = ee + g1.w;
         }
         const float disc = __builtin_fmaf(hb, hb, -(a * c));
-        float sq;
-        if constexpr (kKind == kBig) {
-            // walls are hit by most lanes: no branch around the sqrt
-            const float r = disc * rsqrt_d(disc);
-            sq = disc > 0.0f ? r : 0.0f;
-        } else {
-            sq = sqrt_d(disc);  // a wave whose lanes all miss skips it
-        }
+        // sqrt_d without its branch: disc > 0 gives the same value; disc = +0
+        // gives 0 * inf = NaN inside the Newton steps and fmax(NaN, 0) = 0 =
+        // sqrt_d(0); disc < 0 is rejected below whatever sq is
+        const float sq = __builtin_fmaxf(disc * rsqrt_d(disc), 0.0f);
         const bool neg = hb < 0.0f;
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
@@ -204,18 +211,20 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
         bq = win ? den : bq;
         id = win ? i : id;
     };
-    // index order is kept (ties go to the lowest index): huge-sphere prefix,
-    // then the rest
+    // scan order: axis-anchored walls (x, y, z), general huge spheres, small
+    // spheres; the winner's scan position indexes the shading records, which
+    // the host stores in the same order
     int i = 0;
-    for (; i < A.n_big_prefix; ++i)
+    for (; i < A.end_ax[0]; ++i)
+        test(i, std::integral_constant<int, kAxX>{});
+    for (; i < A.end_ax[1]; ++i)
+        test(i, std::integral_constant<int, kAxY>{});
+    for (; i < A.end_ax[2]; ++i)
+        test(i, std::integral_constant<int, kAxZ>{});
+    for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
-    if (A.big_after) {
-        for (; i < A.n; ++i)
-            test(i, std::integral_constant<int, kEither>{});
-    } else {
-        for (; i < A.n; ++i)
-            test(i, std::integral_constant<int, kSmall>{});
-    }
+    for (; i < A.n; ++i)
+        test(i, std::integral_constant<int, kSmall>{});
     tbest = id >= 0 ? bn / bq : kInf;
     return id;
 }
@@ -820,31 +829,91 @@ bool sphere_ok(const ptg_sphere &s)
     return s.material >= PTG_DIFFUSE && s.material <= PTG_DIELECTRIC;
 }
 
-// Host-side preparation (double -> fp32 records), the counterpart of the
-// oracle's Mode B prep_B; the anchor for huge spheres is the camera position.
+// Anchor of a huge sphere (DESIGN.md "Huge spheres"): the point P = C + R n0
+// of the sphere and its outward normal n0.  The default n0 is the unit vector
+// from C towards the camera.  When the point C + s R e_k of the dominant axis
+// direction of that n0 (k = largest |n0_k|, s = its sign) lies near the scene
+// -- within max(diagonal, 1) of the box around the camera and the non-huge
+// spheres -- that axis point is the anchor instead: any point of the sphere is
+// an exact anchor, and one near the scene keeps |o - P| at scene scale (box
+// walls: the axis points lie inside that box).  Returns k, or -1 for the
+// camera-facing anchor.  The oracle's prep_B makes the same choice
+// (oracle/pt_oracle.c: choose_anchor_B).
+struct SceneBox {
+    double lo[3], hi[3], diag;
+};
+
+int choose_anchor(const ptg_sphere &sp, const ptg_camera *cam, const SceneBox &box, double P[3], double N[3])
+{
+    const double R = sp.radius;
+    double v[3], len2 = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        v[c] = cam->position[c] - sp.position[c];
+        len2 += v[c] * v[c];
+    }
+    const double len = std::sqrt(len2);
+    for (int c = 0; c < 3; ++c)
+        N[c] = len > 0.0 ? v[c] / len : (c == 1 ? 1.0 : 0.0);
+    int k = 0;
+    for (int c = 1; c < 3; ++c)
+        if (std::fabs(N[c]) > std::fabs(N[k]))
+            k = c;
+    const double s = N[k] >= 0.0 ? 1.0 : -1.0;
+    double out2 = 0.0;  // squared distance of the axis point from the scene box
+    for (int c = 0; c < 3; ++c) {
+        const double pa = sp.position[c] + (c == k ? s * R : 0.0);
+        const double o = pa < box.lo[c] ? box.lo[c] - pa : (pa > box.hi[c] ? pa - box.hi[c] : 0.0);
+        out2 += o * o;
+    }
+    const bool snap = std::sqrt(out2) <= std::max(box.diag, 1.0);
+    for (int c = 0; c < 3; ++c) {
+        if (snap)
+            N[c] = c == k ? s : 0.0;
+        P[c] = sp.position[c] + R * N[c];
+    }
+    return snap ? k : -1;
+}
+
+// Box around the camera and every non-huge sphere, and its diagonal.
+SceneBox scene_box(const ptg_sphere *s, int n, const ptg_camera *cam)
+{
+    SceneBox b;
+    for (int c = 0; c < 3; ++c)
+        b.lo[c] = b.hi[c] = cam->position[c];
+    for (int i = 0; i < n; ++i) {
+        if (s[i].radius >= kBigRadius)
+            continue;
+        for (int c = 0; c < 3; ++c) {
+            b.lo[c] = std::min(b.lo[c], s[i].position[c] - s[i].radius);
+            b.hi[c] = std::max(b.hi[c], s[i].position[c] + s[i].radius);
+        }
+    }
+    double d2 = 0.0;
+    for (int c = 0; c < 3; ++c)
+        d2 += (b.hi[c] - b.lo[c]) * (b.hi[c] - b.lo[c]);
+    b.diag = std::sqrt(d2);
+    return b;
+}
+
+// Host-side preparation (double -> fp32 records, scene index order), the
+// counterpart of the oracle's Mode B prep_B.  axis[i] = anchor axis of a huge
+// sphere (-1: camera-facing anchor or not huge).
 void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vector<GeoRec> &geo,
-                   std::vector<ShadeRec> &shade)
+                   std::vector<ShadeRec> &shade, std::vector<int> &axis)
 {
     geo.resize(n);
     shade.resize(n);
+    axis.assign(n, -1);
+    const SceneBox box = scene_box(s, n, cam);
     for (int i = 0; i < n; ++i) {
         const ptg_sphere &sp = s[i];
         const double R = sp.radius;
         GeoRec g;
         if (R >= kBigRadius) {
-            double vx = cam->position[0] - sp.position[0];
-            double vy = cam->position[1] - sp.position[1];
-            double vz = cam->position[2] - sp.position[2];
-            double len = std::sqrt(vx * vx + vy * vy + vz * vz);
-            double nx = 0.0, ny = 1.0, nz = 0.0;
-            if (len > 0.0) {
-                nx = vx / len;
-                ny = vy / len;
-                nz = vz / len;
-            }
-            g.g0 = make_float4((float)(sp.position[0] + R * nx), (float)(sp.position[1] + R * ny),
-                               (float)(sp.position[2] + R * nz), (float)R);
-            g.g1 = make_float4((float)nx, (float)ny, (float)nz, (float)(2.0 * R));
+            double P[3], N[3];
+            axis[i] = choose_anchor(sp, cam, box, P, N);
+            g.g0 = make_float4((float)P[0], (float)P[1], (float)P[2], (float)R);
+            g.g1 = make_float4((float)N[0], (float)N[1], (float)N[2], (float)(2.0 * R));
         } else {
             g.g0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], -1.0f);
             g.g1 = make_float4(0.0f, 0.0f, 0.0f, (float)(-(R * R)));
@@ -870,6 +939,48 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
         r.s2 = make_float4(cx, cy, cz, (float)(1.0 / R));
         r.s3 = make_float4(rx, ry, rz, 0.0f);
         shade[i] = r;
+    }
+}
+
+// Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z,
+// then the other huge spheres, then the small ones, each group in scene index
+// order; end_ax / end_big receive the group ends.
+std::vector<int> scan_order_of(const ptg_sphere *s, int n, const std::vector<int> &axis, KArgs &A)
+{
+    std::vector<int> order;
+    for (int k = 0; k < 3; ++k) {
+        for (int i = 0; i < n; ++i)
+            if (axis[i] == k)
+                order.push_back(i);
+        A.end_ax[k] = (int)order.size();
+    }
+    for (int i = 0; i < n; ++i)
+        if (s[i].radius >= kBigRadius && axis[i] < 0)
+            order.push_back(i);
+    A.end_big = (int)order.size();
+    for (int i = 0; i < n; ++i)
+        if (s[i].radius < kBigRadius)
+            order.push_back(i);
+    return order;
+}
+
+// Records in scan order.  Axis-anchored records carry the signs in their
+// constants: g0.w = s R, g1.w = s 2R (the kernel reads e_k and d_k).
+void prepare_scan_order(const ptg_sphere *s, int n, const std::vector<GeoRec> &geo,
+                        const std::vector<ShadeRec> &shade, const std::vector<int> &axis,
+                        std::vector<GeoRec> &lgeo, std::vector<ShadeRec> &lshade, KArgs &A)
+{
+    lgeo.clear();
+    lshade.clear();
+    for (int i : scan_order_of(s, n, axis, A)) {
+        GeoRec g = geo[i];
+        if (axis[i] >= 0) {
+            const float sgn = (&g.g1.x)[axis[i]];  // +-1 exactly
+            g.g0.w = sgn * g.g0.w;
+            g.g1.w = sgn * g.g1.w;
+        }
+        lgeo.push_back(g);
+        lshade.push_back(shade[i]);
     }
 }
 
@@ -996,9 +1107,16 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         return rc;
     int dev = 0;
     PTG_HIP(hipGetDevice(&dev));
-    std::vector<GeoRec> geo;
-    std::vector<ShadeRec> shade;
-    prepare_scene(spheres, (int)n_spheres, cam, geo, shade);
+    std::vector<GeoRec> geo, lgeo;
+    std::vector<ShadeRec> shade, lshade;
+    std::vector<int> axis;
+    prepare_scene(spheres, (int)n_spheres, cam, geo, shade, axis);
+    KArgs order{};
+    const bool linear = (int)n_spheres <= kLinearMax;
+    if (linear)  // the scan's record order; BVH scenes keep scene index order
+        prepare_scan_order(spheres, (int)n_spheres, geo, shade, axis, lgeo, lshade, order);
+    const std::vector<GeoRec> &up_geo = linear ? lgeo : geo;
+    const std::vector<ShadeRec> &up_shade = linear ? lshade : shade;
     ptg_context *ctx = new ptg_context();
     ctx->device = dev;
     ctx->n = (int)n_spheres;
@@ -1010,18 +1128,17 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the scene failed");
     }
     if (n_spheres) {
-        PTG_HIP(hipMemcpy(ctx->d_geo, geo.data(), n_spheres * sizeof(GeoRec), hipMemcpyHostToDevice));
-        PTG_HIP(hipMemcpy(ctx->d_shade, shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
+        PTG_HIP(hipMemcpy(ctx->d_geo, up_geo.data(), n_spheres * sizeof(GeoRec), hipMemcpyHostToDevice));
+        PTG_HIP(hipMemcpy(ctx->d_shade, up_shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
     }
     KArgs &A = ctx->base;
     std::memset(&A, 0, sizeof(A));
     A.geo = ctx->d_geo;
     A.shade = ctx->d_shade;
     A.n = (int)n_spheres;
-    while (A.n_big_prefix < A.n && spheres[A.n_big_prefix].radius >= kBigRadius)
-        ++A.n_big_prefix;
-    for (int i = A.n_big_prefix; i < A.n; ++i)
-        A.big_after |= spheres[i].radius >= kBigRadius ? 1 : 0;
+    for (int k = 0; k < 3; ++k)
+        A.end_ax[k] = order.end_ax[k];
+    A.end_big = order.end_big;
     if ((int)n_spheres > kLinearMax) {
         BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);
         const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();
@@ -1068,6 +1185,29 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.Y_z = (float)cam->cam_y_axis[2];
     A.lens = (float)cam->lens_radius;
     *out = ctx;
+    return PTG_OK;
+}
+
+int ptg_scene_layout(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int32_t *anchor_axis,
+                     int32_t *scan_order)
+{
+    if (!cam || (n_spheres && (!spheres || !anchor_axis || !scan_order)))
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n_spheres > (size_t)(1 << 24))
+        return fail(PTG_ERR_UNSUPPORTED, "too many spheres");
+    const int n = (int)n_spheres;
+    std::vector<GeoRec> geo;
+    std::vector<ShadeRec> shade;
+    std::vector<int> axis;
+    prepare_scene(spheres, n, cam, geo, shade, axis);
+    for (int i = 0; i < n; ++i)
+        anchor_axis[i] = axis[i];
+    KArgs ends{};
+    std::vector<int> order;
+    if (n <= kLinearMax)
+        order = scan_order_of(spheres, n, axis, ends);
+    for (int i = 0; i < n; ++i)
+        scan_order[i] = n <= kLinearMax ? order[i] : i;
     return PTG_OK;
 }
 

@@ -18,7 +18,7 @@ EXPORTS = (
     "ptg_abi_version", "ptg_last_error", "ptg_device_count", "ptg_render",
     "ptg_context_create", "ptg_context_destroy", "ptg_shard_rows", "ptg_render_device",
     "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
-    "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device",
+    "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device", "ptg_scene_layout",
 )
 
 
@@ -62,6 +62,7 @@ def lib():
             "ptg_reset_accumulation_device": (I, [P, C.POINTER(Params), P]),
             "ptg_accumulate_device": (I, [P, C.POINTER(Params), C.c_int32, C.c_int32, P, P]),
             "ptg_resolve_device": (I, [P, C.POINTER(Params), C.c_int32, P, P]),
+            "ptg_scene_layout": (I, [P, C.c_size_t, P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

@@ -96,6 +96,20 @@ def render(scn, cam, image: np.ndarray, width: int, height: int, samples: int, n
     return image
 
 
+def scene_layout(scn, cam):
+    """Host-side scene preparation (ptg_scene_layout, no device needed): the
+    anchor axis of each huge sphere (-1: camera-facing anchor, or not huge)
+    and the linear scan order (scene indices in the order they are tested)."""
+    sp = _spheres_array(scn)
+    ca = _camera_array(cam)
+    n = len(sp)
+    axis = np.zeros(max(n, 1), dtype=np.int32)
+    order = np.zeros(max(n, 1), dtype=np.int32)
+    check(lib().ptg_scene_layout(sp.ctypes.data, n, ca.ctypes.data, axis.ctypes.data, order.ctypes.data),
+          "ptg_scene_layout")
+    return axis[:n].tolist(), order[:n].tolist()
+
+
 class Context:
     """A scene prepared in HBM on one device (ptg_context)."""
 

@@ -146,6 +146,14 @@ int ptg_unshard_device(const float *d_gathered, float *d_image, int32_t width, i
  * values round(pow(clamp(x), 1/2.2) * 255) of `count` floats. */
 int ptg_tonemap_device(const float *d_image, uint8_t *d_out, size_t count, void *stream);
 
+/* Scene preparation, host only (no device needed): for each sphere the
+ * anchor axis chosen for a huge sphere (0..2; -1 = camera-facing anchor, or
+ * not huge) and the order of the linear scan (scan_order[j] = scene index of
+ * the sphere tested j-th; scenes of <= 64 spheres).  Exact ties between
+ * candidate roots go to the sphere tested first. */
+int ptg_scene_layout(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int32_t *anchor_axis,
+                     int32_t *scan_order);
+
 /* Parity probe: trace individual samples.  d_coords holds n records
  * {x, y, sx, sy, sample} (int32 each); d_out n*3 floats (radiance of that
  * one path, main.cpp:191); d_segs n int32 (scene scans of that path). */

@@ -518,6 +518,7 @@ int po_render_xs_f64(const po_sphere *s, int n, const po_camera *cam, int W, int
 /* Mode B: the float op sequence of the GPU megakernel (DESIGN.md "Mode B")   */
 /* ========================================================================= */
 #define BIG_RADIUS 1000.0
+#define LINEAR_MAX_PREP 64 /* = LINEAR_MAX: scenes scanned linearly on the GPU */
 #define EPSF 1e-4f
 #define INFF 1e20f
 
@@ -544,6 +545,10 @@ static float rsqrt_B(float x)
 }
 /* sqrt(x) = x * rsqrt(x); 0 for x <= 0 */
 static float sqrt_B(float x) { return x > 0.0f ? x * rsqrt_B(x) : 0.0f; }
+/* the linear scan's branch-free form: fmax(x * rsqrt(x), 0).  Equal to
+ * sqrt_B for x > 0 except subnormal x (-inf there -> 0); x = +0 gives
+ * 0 * inf = NaN inside the Newton steps, and fmax(NaN, 0) = 0 */
+static float sqrt_scan_B(float x) { return fmaxf(x * rsqrt_B(x), 0.0f); }
 static f3 fnorm(f3 a)
 {
     float inv = rsqrt_B(fdot(a, a));
@@ -562,6 +567,8 @@ typedef struct {
     f3 emis, col, col_rr;
     float prob;
     int mat;
+    int axis;         /* huge sphere anchored on axis 0..2, else -1 (choose_anchor_B) */
+    int visit;        /* linear scan: the sphere visited at scan position (this element's index) */
 } sphB;
 
 typedef struct {
@@ -569,8 +576,69 @@ typedef struct {
     float lens, invW, invH;
 } camB;
 
+/* Anchor of a huge sphere (DESIGN.md "Huge spheres"): P = C + R n0 on the
+ * sphere, n0 its outward normal there.  Default n0: unit vector from C to the
+ * camera.  If the point C + s R e_k of the dominant axis direction of that n0
+ * lies within max(diagonal, 1) of the box around the camera and the non-huge
+ * spheres, it is the anchor instead (both are exact anchors; the kernel then
+ * reads e_k, d_k instead of two dot products).  Returns k, or -1.  Same
+ * choice as the kernel's host side (ptg_render.hip: choose_anchor). */
+typedef struct { double lo[3], hi[3], diag; } boxB;
+
+static int choose_anchor_B(const po_sphere *sp, const po_camera *cam, const boxB *box, double P[3], double N[3])
+{
+    double R = sp->radius, v[3], len2 = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        v[c] = cam->position[c] - sp->position[c];
+        len2 += v[c] * v[c];
+    }
+    double len = sqrt(len2);
+    for (int c = 0; c < 3; ++c)
+        N[c] = len > 0.0 ? v[c] / len : (c == 1 ? 1.0 : 0.0);
+    int k = 0;
+    for (int c = 1; c < 3; ++c)
+        if (fabs(N[c]) > fabs(N[k]))
+            k = c;
+    double sg = N[k] >= 0.0 ? 1.0 : -1.0, out2 = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        double pa = sp->position[c] + (c == k ? sg * R : 0.0);
+        double o = pa < box->lo[c] ? box->lo[c] - pa : (pa > box->hi[c] ? pa - box->hi[c] : 0.0);
+        out2 += o * o;
+    }
+    int snap = sqrt(out2) <= (box->diag > 1.0 ? box->diag : 1.0);
+    for (int c = 0; c < 3; ++c) {
+        if (snap)
+            N[c] = c == k ? sg : 0.0;
+        P[c] = sp->position[c] + R * N[c];
+    }
+    return snap ? k : -1;
+}
+
+/* box around the camera and every non-huge sphere, and its diagonal */
+static boxB scene_box_B(const po_sphere *s, int n, const po_camera *cam)
+{
+    boxB b;
+    double d2 = 0.0;
+    for (int c = 0; c < 3; ++c)
+        b.lo[c] = b.hi[c] = cam->position[c];
+    for (int i = 0; i < n; ++i) {
+        if (s[i].radius >= BIG_RADIUS)
+            continue;
+        for (int c = 0; c < 3; ++c) {
+            double a = s[i].position[c] - s[i].radius, e = s[i].position[c] + s[i].radius;
+            b.lo[c] = a < b.lo[c] ? a : b.lo[c];
+            b.hi[c] = e > b.hi[c] ? e : b.hi[c];
+        }
+    }
+    for (int c = 0; c < 3; ++c)
+        d2 += (b.hi[c] - b.lo[c]) * (b.hi[c] - b.lo[c]);
+    b.diag = sqrt(d2);
+    return b;
+}
+
 static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
 {
+    boxB box = scene_box_B(s, n, cam);
     for (int i = 0; i < n; ++i) {
         const po_sphere *sp = &s[i];
         sphB *b = &out[i];
@@ -580,20 +648,12 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         b->R2x = (float)(2.0 * R);
         b->negR2 = (float)(-(R * R));
         b->invR = (float)(1.0 / R);
+        b->axis = -1;
         if (b->big) {
-            double vx = cam->position[0] - sp->position[0];
-            double vy = cam->position[1] - sp->position[1];
-            double vz = cam->position[2] - sp->position[2];
-            double len = sqrt(vx * vx + vy * vy + vz * vz);
-            double nx = 0.0, ny = 1.0, nz = 0.0;
-            if (len > 0.0) {
-                nx = vx / len;
-                ny = vy / len;
-                nz = vz / len;
-            }
-            b->P = fk((float)(sp->position[0] + R * nx), (float)(sp->position[1] + R * ny),
-                      (float)(sp->position[2] + R * nz));
-            b->N = fk((float)nx, (float)ny, (float)nz);
+            double P[3], N[3];
+            b->axis = choose_anchor_B(sp, cam, &box, P, N);
+            b->P = fk((float)P[0], (float)P[1], (float)P[2]);
+            b->N = fk((float)N[0], (float)N[1], (float)N[2]);
         } else {
             b->P = fk((float)sp->position[0], (float)sp->position[1], (float)sp->position[2]);
             b->N = fk(0.0f, 0.0f, 0.0f);
@@ -612,6 +672,25 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
             b->col_rr = fk(0.0f, 0.0f, 0.0f);
         }
         b->mat = sp->material;
+    }
+    /* linear scan order (the kernel's record order, ptg_render.hip
+     * prepare_scan_order): x-, y-, z-axis-anchored huge spheres, the other
+     * huge spheres, the small ones; each group in index order */
+    if (n <= LINEAR_MAX_PREP) {
+        int j = 0;
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < n; ++i)
+                if (out[i].big && out[i].axis == k)
+                    out[j++].visit = i;
+        for (int i = 0; i < n; ++i)
+            if (out[i].big && out[i].axis < 0)
+                out[j++].visit = i;
+        for (int i = 0; i < n; ++i)
+            if (!out[i].big)
+                out[j++].visit = i;
+    } else {
+        for (int i = 0; i < n; ++i)
+            out[i].visit = i;
     }
     cb->pos = fk((float)cam->position[0], (float)cam->position[1], (float)cam->position[2]);
     cb->base = fk((float)(cam->lower_left_corner[0] - cam->position[0]),
@@ -668,7 +747,8 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
     float a = fdot(d, d);
     float bn = INFF, bq = 1.0f;
     int id = -1;
-    for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n; ++j) {
+        const int i = s[j].visit; /* scan order: first visited wins exact ties */
         const sphB *sp = &s[i];
         f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
         float ed = fdot(e, d);
@@ -688,7 +768,7 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
         float disc = fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
-        float sq = sqrt_B(disc);
+        float sq = sqrt_scan_B(disc);
         float num, den;
         if (hb < 0.0f) {
             float q = sq - hb; /* > 0; roots c/q (near) and q/a (far) */
@@ -955,6 +1035,21 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
     free(sb);
     if (segments)
         *segments = total;
+    return 0;
+}
+
+int po_scan_layout(const po_sphere *s, int n, const po_camera *cam, int32_t *axis, int32_t *order)
+{
+    if (n < 0)
+        return -1;
+    sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
+    camB cb;
+    prep_B(s, n, cam, sb, &cb);
+    for (int i = 0; i < n; ++i) {
+        axis[i] = sb[i].axis;
+        order[i] = sb[i].visit;
+    }
+    free(sb);
     return 0;
 }
 

@@ -140,6 +140,9 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
                      uint64_t *segments);
 /* One Mode-B path for a given (pixel, sub, sample): returns radiance and
  * segment count -- used by the per-sample GPU parity test. */
+/* Mode B scene layout: anchor axis per sphere (-1: camera-facing anchor or not
+ * huge) and the linear scan order (order[j] = sphere visited j-th) */
+int po_scan_layout(const po_sphere *s, int n, const po_camera *cam, int32_t *axis, int32_t *order);
 int po_sample_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H, int nsub, uint64_t seed,
                   int x, int y, int sx, int sy, uint32_t sample, float out[3]);
 

@@ -72,6 +72,7 @@ def lib():
             "po_render_xs_f32": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P]),
             "po_sample_f32": (I, [P, I, P, I, I, I, U64, I, I, I, I, U32, P]),
             "po_tonemap": (None, [P, C.c_size_t, P]),
+            "po_scan_layout": (I, [P, I, P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -192,3 +193,16 @@ def tonemap(image: np.ndarray) -> np.ndarray:
     out = np.zeros(img.size, dtype=np.int32)
     lib().po_tonemap(ptr(img), img.size, ptr(out))
     return out.reshape(img.shape)
+
+
+def scan_layout(spheres, cam):
+    """Mode B anchor axis per sphere and the linear scan order."""
+    n = len(spheres)
+    axis = np.zeros(max(n, 1), dtype=np.int32)
+    order = np.zeros(max(n, 1), dtype=np.int32)
+    assert lib().po_scan_layout(ptr(spheres), n, ptr(cam), ptr(axis), ptr(order)) == 0
+    return axis[:n].tolist(), order[:n].tolist()
+
+
+def anchor_axes(spheres, cam):
+    return scan_layout(spheres, cam)[0]

@@ -82,9 +82,10 @@ def test_image_bitexact_vs_oracle(name, W, H, samps):
 
 @pytest.mark.parametrize("order", [[5, 6, 7, 0, 1, 2, 3, 4], [0, 5, 1, 6, 2, 7, 3, 4], [7, 6, 5, 4, 3, 2, 1, 0]])
 def test_sphere_order_layouts(order):
-    """The scan runs the leading huge spheres (walls) in their own loop; scenes
-    whose huge spheres come after small ones take the per-record checked loop.
-    Every layout must stay bit-exact (same nearest-hit rule, same tie order)."""
+    """The host regroups the records into scan order (axis-anchored walls by
+    axis, other huge spheres, small spheres); whatever order the scene lists
+    its spheres in, the image stays bit-exact with the oracle, which visits
+    them in the same scan order."""
     _require_gpu()
     W, H, samps = 48, 32, 8
     scn = ptgpu.make_scene("box_mirror", W, H)
@@ -95,6 +96,27 @@ def test_sphere_order_layouts(order):
     ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
     _check_equal(gpu, ref)
     assert gsegs == rsegs
+
+
+def test_tilted_huge_spheres_take_the_general_anchor():
+    """Huge spheres whose camera-facing point is far from every axis point
+    (a 45-degree wall) keep the general anchored form; mixed with the axis
+    walls and listed after small spheres, the image stays bit-exact."""
+    _require_gpu()
+    W, H, samps = 48, 32, 8
+    scn = ptgpu.make_scene("box", W, H)
+    R = 1e6
+    k = R / 2 ** 0.5
+    tilted = ptgpu.sphere(R, (k + 0.3, 0.0, -k - 0.3), (0.0, 0.0, 0.0), (0.2, 0.6, 0.6),
+                          ptgpu.reflection_type.specular)
+    scn.spheres = scn.spheres[5:] + [tilted] + scn.spheres[:5]
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    gpu, gsegs = _gpu_image(scn, cam, W, H, samps, count_segments=True)
+    sp, ca = _oracle_scene(scn, cam)
+    ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
+    _check_equal(gpu, ref)
+    assert gsegs == rsegs
+    assert po.anchor_axes(sp, ca) == [-1, -1, -1, -1, 0, 0, 2, 1, 1]
 
 
 @pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:3000"])

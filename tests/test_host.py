@@ -109,6 +109,36 @@ def test_abi_rejects_bad_arguments_without_gpu_work():
         ptgpu.Context(bad, cam)
 
 
+def _tilted_box():
+    scn = ptgpu.make_scene("box", 64, 48)
+    R = 1e6
+    k = R / 2 ** 0.5
+    tilted = ptgpu.sphere(R, (k + 0.3, 0.0, -k - 0.3), (0.0, 0.0, 0.0), (0.2, 0.6, 0.6),
+                          ptgpu.reflection_type.specular)
+    scn.spheres = scn.spheres[5:] + [tilted] + scn.spheres[:5]
+    return scn
+
+
+@pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:40", "synthetic:300", "tilted"])
+def test_scene_layout_matches_oracle(name):
+    """The kernel host's anchor choice and scan order (ptg_scene_layout, no GPU)
+    equal the oracle's Mode B preparation: the box walls take the axis
+    anchors, a 45-degree huge sphere keeps the camera-facing anchor."""
+    scn = _tilted_box() if name == "tilted" else ptgpu.make_scene(name, 64, 48)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    axis, order = ptgpu.scene_layout(scn, cam)
+    sp = scn.to_array().view(po.SPHERE_DT)
+    ca = cam.to_array().view(po.CAMERA_DT)
+    assert (axis, order) == po.scan_layout(sp, ca)
+    assert sorted(order) == list(range(len(scn.spheres)))
+    if name in ("box", "box_mirror"):
+        assert axis == [0, 0, 2, 1, 1, -1, -1, -1] and order == [0, 1, 3, 4, 2, 5, 6, 7]
+    if name == "tilted":
+        assert axis == [-1, -1, -1, -1, 0, 0, 2, 1, 1] and order == [4, 5, 7, 8, 6, 3, 0, 1, 2]
+    if name == "simple":  # no huge sphere: index order
+        assert axis == [-1] * 5 and order == list(range(5))
+
+
 def test_params_struct_matches_header():
     assert C.sizeof(ptgpu.Params) == 48
     p = ptgpu.make_params(1920, 1080, 256)
