@@ -70,43 +70,64 @@ __device__ __forceinline__ uint32_t sample_state(uint64_t key, uint32_t sample)
     uint32_t st = (uint32_t)(mix64(key + ((uint64_t)sample + 1ull) * 0x9E3779B97F4A7C15ull) >> 32);
     return st ? st : 0x6D2B79F5u;
 }
-// one U[0,1) draw: xorshift32 (13,17,5), top 24 bits
-__device__ __forceinline__ float draw(uint32_t &st)
+// one draw: xorshift32 (13,17,5); its top 24 bits m give U[0,1) = m * 2^-24
+__device__ __forceinline__ uint32_t draw_bits(uint32_t &st)
 {
     st ^= st << 13;
     st ^= st >> 17;
     st ^= st << 5;
-    return (float)(st >> 8) * 0x1p-24f;
+    return st >> 8;
+}
+__device__ __forceinline__ float draw(uint32_t &st) { return (float)draw_bits(st) * 0x1p-24f; }
+
+// sin/cos of 2*pi*u (replaces libm at main.cpp:55) for u = m * 2^-24, m the
+// draw's 24-bit integer: a 128-entry table of cos/sin(2*pi*k/128) (LDS,
+// trig_table below) indexed by the top 7 bits, rotated by the remaining angle
+// dl = 2*pi*(m mod 2^17)*2^-24 < 2*pi/128 with sin dl = dl (1 - dl^2/6) and
+// cos dl = 1 - dl^2/2 + dl^4/24 (truncation < 3e-9).  14 VALU instead of the
+// ~30 of a quadrant-split degree-13 polynomial.
+constexpr int kTrigBits = 7;
+constexpr int kTrigEntries = 1 << kTrigBits;
+__device__ __forceinline__ void sincos2pi_tab(uint32_t m, const float2 *tab, float &c, float &s)
+{
+    const float2 cs = tab[m >> (24 - kTrigBits)];
+    const float dl = (float)(m & ((1u << (24 - kTrigBits)) - 1u)) * 0x1.921fb6p-22f;  // 2*pi*2^-24
+    const float d2 = dl * dl;
+    const float sd = dl * __builtin_fmaf(d2, -0x1.555556p-3f, 1.0f);
+    const float cd = __builtin_fmaf(d2, __builtin_fmaf(d2, 0x1.555556p-5f, -0.5f), 1.0f);
+    c = __builtin_fmaf(cs.x, cd, -(cs.y * sd));
+    s = __builtin_fmaf(cs.y, cd, cs.x * sd);
 }
 
-// sin/cos of 2*pi*u, u in [0,1) (replaces libm at main.cpp:55): exact quadrant
-// split of 4u, Taylor polynomials of sin(pi/2 f) / cos(pi/2 f), f in [0,1).
-__device__ __forceinline__ void sincos2pi(float u, float &c, float &s)
+// Host: the table, {cos, sin}(2*pi*k/128) rounded to float.  Taylor series in
+// double on the first octant (fixed operation order, no libm) and exact
+// symmetries elsewhere, so the oracle's copy (oracle/pt_oracle.c:
+// trig_table_B) is the same bit for bit on any IEEE-754 host.
+inline void trig_table(float *tab /* 2 * kTrigEntries */)
 {
-    float v = u * 4.0f;
-    float qf = __builtin_floorf(v);
-    float f = v - qf;
-    int q = (int)qf & 3;
-    float f2 = f * f;
-    float ps = __builtin_fmaf(f2, 0x1.e8f434p-25f, -0x1.e3075p-19f);
-    ps = __builtin_fmaf(f2, ps, 0x1.507834p-13f);
-    ps = __builtin_fmaf(f2, ps, -0x1.32d2ccp-8f);
-    ps = __builtin_fmaf(f2, ps, 0x1.466bc6p-4f);
-    ps = __builtin_fmaf(f2, ps, -0x1.4abbcep-1f);
-    ps = __builtin_fmaf(f2, ps, 0x1.921fb6p+0f);
-    float sn = f * ps;
-    float pc = __builtin_fmaf(f2, -0x1.b6e25p-28f, 0x1.f9d38ap-22f);
-    pc = __builtin_fmaf(f2, pc, -0x1.a6d1f2p-16f);
-    pc = __builtin_fmaf(f2, pc, 0x1.e1f506p-11f);
-    pc = __builtin_fmaf(f2, pc, -0x1.55d3c8p-6f);
-    pc = __builtin_fmaf(f2, pc, 0x1.03c1fp-2f);
-    pc = __builtin_fmaf(f2, pc, -0x1.3bd3ccp+0f);
-    float cs = __builtin_fmaf(f2, pc, 1.0f);
-    // rotate by q quarter turns
-    float c1 = (q & 1) ? -sn : cs;
-    float s1 = (q & 1) ? cs : sn;
-    c = (q & 2) ? -c1 : c1;
-    s = (q & 2) ? -s1 : s1;
+    const double pi = 3.14159265358979323846;
+    constexpr int kOct = kTrigEntries / 8, kQuad = kTrigEntries / 4;
+    double bc[kOct + 1], bs[kOct + 1];
+    for (int r = 0; r <= kOct; ++r) {
+        const double a = 2.0 * pi / (double)kTrigEntries * (double)r, a2 = a * a;
+        double ts = a, ss = a, tc = 1.0, sc = 1.0;
+        for (int n = 1; n <= 12; ++n) {
+            ts = -ts * a2 / (double)((2 * n) * (2 * n + 1));
+            ss = ss + ts;
+            tc = -tc * a2 / (double)((2 * n - 1) * (2 * n));
+            sc = sc + tc;
+        }
+        bc[r] = sc;
+        bs[r] = ss;
+    }
+    for (int k = 0; k < kTrigEntries; ++k) {
+        const int q = k / kQuad, r = k % kQuad;
+        const double c0 = r <= kOct ? bc[r] : bs[kQuad - r], s0 = r <= kOct ? bs[r] : bc[kQuad - r];
+        const double c = q == 0 ? c0 : (q == 1 ? -s0 : (q == 2 ? -c0 : s0));
+        const double s = q == 0 ? s0 : (q == 1 ? c0 : (q == 2 ? -s0 : -c0));
+        tab[2 * k] = (float)c;
+        tab[2 * k + 1] = (float)s;
+    }
 }
 
 // Scene records prepared on the host (ptg_render.hip: prepare_scene).

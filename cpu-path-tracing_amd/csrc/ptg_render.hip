@@ -93,6 +93,7 @@ struct KArgs {
     const GeoRec *big_geo;    // huge spheres, tested linearly
     const int *big_id;
     int n_nodes, n_big;
+    const float2 *trig;  // {cos, sin}(2 pi k / 128), staged in LDS (sincos2pi_tab)
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
     float pos_x, pos_y, pos_z;
     float base_x, base_y, base_z;
@@ -339,8 +340,8 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
 template <bool kBvh, bool kCount = false>
-__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const ShadeRec *shade, f3 &o, f3 &d, f3 &T,
-                                        f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
+__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const ShadeRec *shade, const float2 *trig,
+                                        f3 &o, f3 &d, f3 &T, f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
 {
     float t;
     int id;
@@ -388,9 +389,9 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const
     const bool isG = mat == PTG_DIELECTRIC;
     float cp = 0.0f, sp = 0.0f, ra = 0.0f;
     if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
-        float u_phi = draw(st);
+        const uint32_t m_phi = draw_bits(st);
         ra = draw(st);
-        sincos2pi(u_phi, cp, sp);
+        sincos2pi_tab(m_phi, trig, cp, sp);
     }
     // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
     f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
@@ -489,15 +490,19 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     ShadeRec *lds_shade = reinterpret_cast<ShadeRec *>(dyn_lds + (size_t)A.n * sizeof(GeoRec));
     const GeoRec *geo = A.geo;
     const ShadeRec *shade = A.shade;
+    __shared__ float2 lds_trig[kTrigEntries];
+    static_assert(kTrigEntries <= kBlock, "one table entry per thread");
+    if (threadIdx.x < kTrigEntries)
+        lds_trig[threadIdx.x] = A.trig[threadIdx.x];
     if constexpr (kLdsGeo) {
         for (int i = threadIdx.x; i < A.n; i += kBlock) {
             lds_geo[i] = A.geo[i];
             lds_shade[i] = A.shade[i];
         }
-        __syncthreads();
         geo = lds_geo;
         shade = lds_shade;
     }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler keep all
     // per-unit bookkeeping in SGPRs
@@ -613,7 +618,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            if (segment<kBvh, kCount>(A, geo, shade, o, d, T, E, depth, st, scnt)) {
+            if (segment<kBvh, kCount>(A, geo, shade, lds_trig, o, d, T, E, depth, st, scnt)) {
                 item = -1;
                 if (has_pre) {
                     pe_x = E.x;
@@ -771,7 +776,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     while (!done) {
         segs += 1;
         ScanCount scnt;
-        done = segment<kBvh>(A, A.geo, A.shade, o, d, T, E, depth, st, scnt);
+        done = segment<kBvh>(A, A.geo, A.shade, A.trig, o, d, T, E, depth, st, scnt);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -812,6 +817,7 @@ struct ptg_context {
     GeoRec *d_geo;
     ShadeRec *d_shade;
     void *d_bvh;  // one allocation: nodes | leaf geometry | leaf ids | big geometry | big ids
+    float2 *d_trig;  // sin/cos table (trig_table)
     unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
     size_t acc_elems;
     KArgs base;  // camera + scene fields filled
@@ -1131,8 +1137,18 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         PTG_HIP(hipMemcpy(ctx->d_geo, up_geo.data(), n_spheres * sizeof(GeoRec), hipMemcpyHostToDevice));
         PTG_HIP(hipMemcpy(ctx->d_shade, up_shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
     }
+    {
+        float tab[2 * kTrigEntries];
+        trig_table(tab);
+        if (hipMalloc(&ctx->d_trig, sizeof(tab)) != hipSuccess) {
+            ptg_context_destroy(ctx);
+            return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the sin/cos table failed");
+        }
+        PTG_HIP(hipMemcpy(ctx->d_trig, tab, sizeof(tab), hipMemcpyHostToDevice));
+    }
     KArgs &A = ctx->base;
     std::memset(&A, 0, sizeof(A));
+    A.trig = ctx->d_trig;
     A.geo = ctx->d_geo;
     A.shade = ctx->d_shade;
     A.n = (int)n_spheres;
@@ -1218,6 +1234,8 @@ int ptg_context_destroy(ptg_context *ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_shade);
+    if (ctx->d_trig)
+        (void)hipFree(ctx->d_trig);
     if (ctx->d_bvh)
         (void)hipFree(ctx->d_bvh);
     if (ctx->d_acc)

@@ -518,6 +518,8 @@ int po_render_xs_f64(const po_sphere *s, int n, const po_camera *cam, int W, int
 /* Mode B: the float op sequence of the GPU megakernel (DESIGN.md "Mode B")   */
 /* ========================================================================= */
 #define BIG_RADIUS 1000.0
+#define TRIG_BITS 7 /* sin/cos table of 2^TRIG_BITS entries (sincos2pi_B) */
+#define TRIG_ENTRIES (1 << TRIG_BITS)
 #define LINEAR_MAX_PREP 64 /* = LINEAR_MAX: scenes scanned linearly on the GPU */
 #define EPSF 1e-4f
 #define INFF 1e20f
@@ -574,6 +576,7 @@ typedef struct {
 typedef struct {
     f3 pos, base, X, Y; /* base = float(llc - pos) */
     float lens, invW, invH;
+    float trig[2 * TRIG_ENTRIES]; /* sincos2pi_B table */
 } camB;
 
 /* Anchor of a huge sphere (DESIGN.md "Huge spheres"): P = C + R n0 on the
@@ -635,6 +638,8 @@ static boxB scene_box_B(const po_sphere *s, int n, const po_camera *cam)
     b.diag = sqrt(d2);
     return b;
 }
+
+static void trig_table_B(float *tab);
 
 static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
 {
@@ -699,38 +704,55 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
     cb->X = fk((float)cam->cam_x_axis[0], (float)cam->cam_x_axis[1], (float)cam->cam_x_axis[2]);
     cb->Y = fk((float)cam->cam_y_axis[0], (float)cam->cam_y_axis[1], (float)cam->cam_y_axis[2]);
     cb->lens = (float)cam->lens_radius;
+    trig_table_B(cb->trig);
     cb->invW = 0.0f;
     cb->invH = 0.0f;
 }
 
-/* sin/cos of 2*pi*u for u in [0,1): quadrant split of 4u (exact) and Taylor
- * polynomials of sin(pi/2 f), cos(pi/2 f) on f in [0,1) (replaces libm in
- * main.cpp:55 so host and device agree bit-for-bit). */
-static void sincos2pi_B(float u, float *c, float *s)
+/* sin/cos of 2*pi*u, u = m * 2^-24 with m the draw's 24-bit integer (replaces
+ * libm in main.cpp:55 so host and device agree bit-for-bit): table entry
+ * {cos, sin}(2*pi*k/128) for k = m >> 17, rotated by dl = 2*pi*(m mod 2^17)*2^-24
+ * with sin dl = dl (1 - dl^2/6), cos dl = 1 - dl^2/2 + dl^4/24 (truncation
+ * < 3e-9).  Kernel: pt_device.hpp sincos2pi_tab. */
+
+static void sincos2pi_B(uint32_t m, const float *tab, float *c, float *s)
 {
-    float v = u * 4.0f;
-    float qf = floorf(v);
-    float f = v - qf;
-    int q = (int)qf & 3;
-    float f2 = f * f;
-    float ps = fmaf(f2, 0x1.e8f434p-25f, -0x1.e3075p-19f);
-    ps = fmaf(f2, ps, 0x1.507834p-13f);
-    ps = fmaf(f2, ps, -0x1.32d2ccp-8f);
-    ps = fmaf(f2, ps, 0x1.466bc6p-4f);
-    ps = fmaf(f2, ps, -0x1.4abbcep-1f);
-    ps = fmaf(f2, ps, 0x1.921fb6p+0f);
-    float sn = f * ps;
-    float pc = fmaf(f2, -0x1.b6e25p-28f, 0x1.f9d38ap-22f);
-    pc = fmaf(f2, pc, -0x1.a6d1f2p-16f);
-    pc = fmaf(f2, pc, 0x1.e1f506p-11f);
-    pc = fmaf(f2, pc, -0x1.55d3c8p-6f);
-    pc = fmaf(f2, pc, 0x1.03c1fp-2f);
-    pc = fmaf(f2, pc, -0x1.3bd3ccp+0f);
-    float cs = fmaf(f2, pc, 1.0f);
-    float rc = (q == 0) ? cs : (q == 1) ? -sn : (q == 2) ? -cs : sn;
-    float rs = (q == 0) ? sn : (q == 1) ? cs : (q == 2) ? -sn : -cs;
-    *c = rc;
-    *s = rs;
+    const float *cs = tab + 2 * (m >> (24 - TRIG_BITS));
+    float dl = (float)(m & ((1u << (24 - TRIG_BITS)) - 1u)) * 0x1.921fb6p-22f;
+    float d2 = dl * dl;
+    float sd = dl * fmaf(d2, -0x1.555556p-3f, 1.0f);
+    float cd = fmaf(d2, fmaf(d2, 0x1.555556p-5f, -0.5f), 1.0f);
+    *c = fmaf(cs[0], cd, -(cs[1] * sd));
+    *s = fmaf(cs[1], cd, cs[0] * sd);
+}
+
+/* The table: Taylor series in double on the first octant (fixed operation
+ * order, no libm), exact symmetries elsewhere, rounded to float. */
+static void trig_table_B(float *tab)
+{
+    const double pi = 3.14159265358979323846;
+    enum { OCT = TRIG_ENTRIES / 8, QUAD = TRIG_ENTRIES / 4 };
+    double bc[OCT + 1], bs[OCT + 1];
+    for (int r = 0; r <= OCT; ++r) {
+        double a = 2.0 * pi / (double)TRIG_ENTRIES * (double)r, a2 = a * a;
+        double ts = a, ss = a, tc = 1.0, sc = 1.0;
+        for (int n = 1; n <= 12; ++n) {
+            ts = -ts * a2 / (double)((2 * n) * (2 * n + 1));
+            ss = ss + ts;
+            tc = -tc * a2 / (double)((2 * n - 1) * (2 * n));
+            sc = sc + tc;
+        }
+        bc[r] = sc;
+        bs[r] = ss;
+    }
+    for (int k = 0; k < TRIG_ENTRIES; ++k) {
+        int q = k / QUAD, r = k % QUAD;
+        double c0 = r <= OCT ? bc[r] : bs[QUAD - r], s0 = r <= OCT ? bs[r] : bc[QUAD - r];
+        double c = q == 0 ? c0 : (q == 1 ? -s0 : (q == 2 ? -c0 : s0));
+        double s = q == 0 ? s0 : (q == 1 ? c0 : (q == 2 ? -s0 : -c0));
+        tab[2 * k] = (float)c;
+        tab[2 * k + 1] = (float)s;
+    }
 }
 
 /* Scene scan, Mode B (main.cpp:30-42 + sphere.cpp:6-30 with the stable
@@ -912,10 +934,10 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y
         T = fk(T.x * col.x, T.y * col.y, T.z * col.z);
         int reflect = 0;
         if (sp->mat == 0) { /* diffuse, main.cpp:44-58 */
-            float u_phi = po_xs_f32(&st);
+            uint32_t m_phi = po_xorshift32(&st) >> 8;
             float ra = po_xs_f32(&st);
             float cp, sp_;
-            sincos2pi_B(u_phi, &cp, &sp_);
+            sincos2pi_B(m_phi, cam->trig, &cp, &sp_);
             float sth = sqrt_B(ra);
             float cth = sqrt_B(1.0f - ra);
             f3 w = nn;
@@ -1036,6 +1058,14 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
     if (segments)
         *segments = total;
     return 0;
+}
+
+void po_sincos2pi(const uint32_t *m, size_t n, float *out)
+{
+    float tab[2 * TRIG_ENTRIES];
+    trig_table_B(tab);
+    for (size_t i = 0; i < n; ++i)
+        sincos2pi_B(m[i] & 0xFFFFFFu, tab, &out[2 * i], &out[2 * i + 1]);
 }
 
 int po_scan_layout(const po_sphere *s, int n, const po_camera *cam, int32_t *axis, int32_t *order)

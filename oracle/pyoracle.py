@@ -73,6 +73,7 @@ def lib():
             "po_sample_f32": (I, [P, I, P, I, I, I, U64, I, I, I, I, U32, P]),
             "po_tonemap": (None, [P, C.c_size_t, P]),
             "po_scan_layout": (I, [P, I, P, P, P]),
+            "po_sincos2pi": (None, [P, C.c_size_t, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -206,3 +207,11 @@ def scan_layout(spheres, cam):
 
 def anchor_axes(spheres, cam):
     return scan_layout(spheres, cam)[0]
+
+
+def sincos2pi(m):
+    """Mode B {cos, sin}(2 pi m / 2^24) for 24-bit integers m."""
+    m = np.ascontiguousarray(m, dtype=np.uint32)
+    out = np.zeros((m.size, 2), dtype=np.float32)
+    lib().po_sincos2pi(ptr(m), m.size, ptr(out))
+    return out
