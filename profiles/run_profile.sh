@@ -7,6 +7,7 @@
 #   pass 1: --pmc FETCH_SIZE            (HBM read bytes; x2 on gfx950 for wide streams, MI355X_MICROARCH.md HBM)
 #   pass 2: --pmc WRITE_SIZE            (HBM write bytes)
 #   pass 3: --pmc SQ instruction mix    (VALU/SALU/SMEM/LDS instruction and cycle counts)
+#   pass 5: --pmc GRBM_GUI_ACTIVE + SQ  (clock, VALUBusy, VALU lane utilisation, occupancy)
 set -euo pipefail
 tag=${1:-r01}
 shift || true
@@ -19,4 +20,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-for
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_write.json" 2> "$out/write.err"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY -d "$out/sq" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_sq.json" 2> "$out/sq.err"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SMEM -d "$out/sq2" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_sq2.json" 2> "$out/sq2.err"
+timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$out/busy" -o run --output-format csv -- python3 "${BENCH[@]}" > "$out/bench_busy.json" 2> "$out/busy.err"
 echo "profile $tag done"

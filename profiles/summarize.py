@@ -56,6 +56,24 @@ def main(src, tag, kernel_sub="render_kernel"):
         segs = b["roofline"]["segments_per_sample"] * samples
         if "SQ_INSTS_VALU" in sq:
             out["valu_insts_per_segment_wave_level"] = sq["SQ_INSTS_VALU"] * 64 / segs
+    busyp = os.path.join(src, "busy", "run_counter_collection.csv")
+    if os.path.exists(busyp):
+        bz, _ = per_kernel(busyp, kernel_sub)
+        out["busy"] = bz
+        grbm = bz.get("GRBM_GUI_ACTIVE", 0.0)
+        if grbm > 0:
+            cu = 256
+            # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs' GRBM instances
+            cyc = grbm / 8 if grbm / (out["render_avg_ms"] * 1e-3) > 4e9 else grbm
+            out["derived"] = {
+                "clock_GHz": cyc / (out["render_avg_ms"] * 1e-3) / 1e9,
+                # rocprof's VALUBusy (counter_defs.yaml): SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE
+                "VALUBusy_pct": 100.0 * bz["SQ_ACTIVE_INST_VALU"] / cu / cyc,
+                # issue view: wave64 VALU instructions x 2 cycles (SIMD-32) over the 1,024 SIMDs' cycles
+                "valu_issue_pct": 100.0 * bz["SQ_INSTS_VALU"] * 2 / (4 * cu) / cyc,
+                "VALUUtilization_pct": 100.0 * bz["SQ_THREAD_CYCLES_VALU"] / (bz["SQ_ACTIVE_INST_VALU"] * 64),
+                "MeanOccupancyPerCU_waves": bz["SQ_WAVE_CYCLES"] / cyc / cu,
+            }
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{tag}_summary.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
