@@ -70,6 +70,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_REFILL_BATCH
 #define PTG_REFILL_BATCH 32  // measured: 32 beats 16 and ties 48 (DESIGN.md perf log)
 #endif
+#ifndef PTG_PARK_LDS
+#define PTG_PARK_LDS 1  // park finished paths in the lane's LDS record instead of registers
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -369,17 +372,13 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const
     f3 nn = front ? on : mk3(-on.x, -on.y, -on.z);
     // main.cpp:126
     E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
-    // main.cpp:128-139: Russian roulette after depth 4
-    float4 col;
-    if (depth > kRRThreshold) {
-        if (draw(st) < s0.w)
-            col = S.s3;
-        else
-            return true;
-    } else {
-        col = S.s2;
-    }
-    T = mk3(T.x * col.x, T.y * col.y, T.z * col.z);
+    // main.cpp:128-139: Russian roulette after depth 4.  Both colour records
+    // are loaded and selected (3 selects instead of address arithmetic)
+    const float4 c2 = S.s2, c3 = S.s3;
+    const bool rr = depth > kRRThreshold;
+    if (rr && !(draw(st) < s0.w))
+        return true;
+    T = mk3(T.x * (rr ? c3.x : c2.x), T.y * (rr ? c3.y : c2.y), T.z * (rr ? c3.z : c2.z));
     // BRDF samplers (main.cpp:44-97).  Diffuse and dielectric lanes share the
     // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
     // holding both materials issues them once; every lane's arithmetic is the
@@ -605,6 +604,76 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         atomicAdd(&lds_acc[wv][sl + 64], quant(ey));
         atomicAdd(&lds_acc[wv][sl + 128], quant(ez));
     };
+#if PTG_PARK_LDS
+    // A finished path parks its radiance (E, slot) in the lane's LDS record
+    // lds_pre[wv][lane], which just gave up its prefetched ray; the quantise +
+    // LDS adds run for all parked lanes at the next refill batch (before the
+    // refill writes new prefetched rays there).  A lane that finishes again
+    // before the batch has no prefetched ray: it waits (E in registers),
+    // which forces a batch; there its E is parked, and it starts a new ray.
+    bool parked = false;
+    auto park = [&]() {
+        lds_pre[wv][lane][0] = make_float4(E.x, E.y, E.z, __int_as_float(slot));
+        parked = true;
+    };
+    auto flush_parked = [&]() {
+        const float4 pk = lds_pre[wv][lane][0];
+        flush(pk.x, pk.y, pk.z, __float_as_int(pk.w));
+        parked = false;
+    };
+    for (;;) {
+        if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+            break;
+        if (item >= 0) {
+            if constexpr (kCount)
+                segs += 1;
+            if (segment<kBvh, kCount>(A, geo, shade, lds_trig, o, d, T, E, depth, st, scnt)) {
+                item = -1;
+                if (has_pre) {
+                    const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
+                    park();
+                    begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x),
+                          __float_as_uint(p1.y));
+                    has_pre = false;
+                } else {
+                    waiting = true;  // E is kept until the batch
+                }
+            }
+        }
+        if (next < total) {
+            const unsigned long long need = __ballot(!has_pre);
+            const int nn = (int)__popcll(need);
+            if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
+                const bool idle = waiting || item < 0;
+                if (parked)
+                    flush_parked();
+                if (waiting)
+                    park();
+                waiting = false;
+                if (!has_pre) {
+                    const int ni = next + (int)__popcll(need & ((1ull << lane) - 1ull));
+                    if (ni < total) {
+                        f3 ro, rd;
+                        uint32_t rs;
+                        ray_of(ni, ro, rd, rs);
+                        if (idle) {  // idle lane: start it now (its record may hold a parked path)
+                            begin(ni, ro, rd, rs);
+                        } else {
+                            store_pre(ni, ro, rd, rs);
+                            has_pre = true;
+                        }
+                    }
+                }
+                next += nn;
+            }
+        } else if (waiting) {  // pool exhausted: nothing left for this lane
+            flush(E.x, E.y, E.z, slot);
+            waiting = false;
+        }
+    }
+    if (parked)
+        flush_parked();
+#else
     // A finished path parks its radiance in registers (pe, pslot); the
     // quantise + LDS adds run for all parked lanes at the next refill batch,
     // not in every iteration in which some lane finishes.  A lane parks at
@@ -672,6 +741,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     }
     if (pslot >= 0)
         flush(pe_x, pe_y, pe_z, pslot);
+#endif
     if constexpr (kCount) {
         unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes;
         for (int off = 32; off > 0; off >>= 1) {
