@@ -50,7 +50,7 @@ inline int render_image(scene const &scn, camera const &cam, std::vector<vec3> &
     p.samples = samps;
     p.num_subpixels = num_subpixels;
     p.seed = seed;
-    p.band_rows = 8;
+    p.band_rows = 1;  // single-row bands: equal shards whenever shard_count divides H
     p.shard_rank = 0;
     p.shard_count = 1;
     return ptg_render(reinterpret_cast<ptg_sphere const *>(scn.spheres.data()), scn.spheres.size(),

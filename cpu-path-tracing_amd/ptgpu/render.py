@@ -23,7 +23,7 @@ from ._abi import Params, check, lib
 from .scene import CAMERA_DT, SPHERE_DT, camera, scene
 
 DEFAULT_SEED = 0x5EED0001
-DEFAULT_BAND_ROWS = 8
+DEFAULT_BAND_ROWS = 1  # single-row bands: equal shards whenever N divides H (tools/shard_sim.py: 8-way 95.8 % vs 94.4 % with 8-row bands)
 
 
 def _spheres_array(scn) -> np.ndarray:

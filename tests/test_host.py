@@ -142,4 +142,4 @@ def test_scene_layout_matches_oracle(name):
 def test_params_struct_matches_header():
     assert C.sizeof(ptgpu.Params) == 48
     p = ptgpu.make_params(1920, 1080, 256)
-    assert (p.width, p.height, p.samples, p.num_subpixels, p.band_rows, p.shard_count) == (1920, 1080, 256, 2, 8, 1)
+    assert (p.width, p.height, p.samples, p.num_subpixels, p.band_rows, p.shard_count) == (1920, 1080, 256, 2, 1, 1)
