@@ -40,8 +40,23 @@ __device__ __forceinline__ float rsqrt_d(float x)
     t = __builtin_fmaf(-h, t, 1.5f);
     return y * t;
 }
-// sqrt(x) = x * rsqrt(x); 0 for x <= 0
-__device__ __forceinline__ float sqrt_d(float x) { return x > 0.0f ? x * rsqrt_d(x) : 0.0f; }
+// Deterministic square root for x >= 0 (x = +0 gives 0): the same bit-trick
+// seed y ~ 1/sqrt(x), then two coupled Goldschmidt steps on g ~ sqrt(x) and
+// h ~ 1/(2 sqrt(x)) -- 9 VALU, relative error ~1e-6, no special case for 0.
+// The oracle's sqrt_gs_B executes the same operations.
+__device__ __forceinline__ float sqrt_gs(float x)
+{
+    const float y = __uint_as_float(0x5f375a86u - (__float_as_uint(x) >> 1));
+    float g = x * y;
+    float h = 0.5f * y;
+    float r = __builtin_fmaf(-g, h, 0.5f);
+    g = __builtin_fmaf(g, r, g);
+    h = __builtin_fmaf(h, r, h);
+    r = __builtin_fmaf(-g, h, 0.5f);
+    return __builtin_fmaf(g, r, g);
+}
+// sqrt for any x: 0 for x <= 0
+__device__ __forceinline__ float sqrt_d(float x) { return sqrt_gs(__builtin_fmaxf(x, 0.0f)); }
 // vec.cpp:35-38: x * (1 / sqrt(x.x))
 __device__ __forceinline__ f3 norm3(f3 a)
 {
@@ -144,6 +159,14 @@ struct GeoRec {
 };
 struct ShadeRec {
     float4 s0, s1, s2, s3;
+};
+// Linear scenes: one 96-B record per sphere in scan order (geometry, then
+// shading), plus a sentinel record at index n that stands for "no hit": the
+// scan tracks the winner by its record address (the LDS address it already
+// holds for the broadcast reads) instead of by an index.
+struct LinRec {
+    GeoRec g;
+    ShadeRec s;
 };
 
 }  // namespace ptg

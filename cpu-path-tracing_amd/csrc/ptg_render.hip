@@ -70,9 +70,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_REFILL_BATCH
 #define PTG_REFILL_BATCH 32  // measured: 32 beats 16 and ties 48 (DESIGN.md perf log)
 #endif
-#ifndef PTG_PARK_LDS
-#define PTG_PARK_LDS 1  // park finished paths in the lane's LDS record instead of registers
-#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -80,8 +77,8 @@ constexpr int kWavesPerBlock = kBlock / 64;
 constexpr double kBigRadius = 1000.0;
 
 struct KArgs {
-    const GeoRec *geo;
-    const ShadeRec *shade;
+    const LinRec *lin;      // linear scenes (<= kLinearMax): n records in scan order + sentinel
+    const ShadeRec *shade;  // BVH scenes: shading records in scene index order
     int n;
     // linear scenes: records in SCAN order (prepare_scan_order), grouped by
     // kind: [0, end_ax[0]) huge spheres anchored on the x axis, then y, then z
@@ -172,17 +169,19 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4 };
 
 __device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
-__device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 o, f3 d, float &tbest)
+// Returns the winner's record, or the sentinel recs + n (no hit).
+__device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec *recs, f3 o, f3 d, float &tbest)
 {
     // the nearest root is kept as a fraction bn/bq (bq > 0); candidates are
     // compared by cross-multiplication, only the winner is divided
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
-    int id = -1;
+    const LinRec *best = recs + A.n;
     auto test = [&](const int i, auto kind_tag) {
         constexpr int kKind = decltype(kind_tag)::value;
-        float4 g0 = geo[i].g0;
-        float4 g1 = geo[i].g1;
+        const LinRec *r = recs + i;
+        float4 g0 = r->g.g0;
+        float4 g1 = r->g.g1;
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
         float ed = dot3(e, d);
         float ee = dot3(e, e);
@@ -198,10 +197,8 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
             c = ee + g1.w;
         }
         const float disc = __builtin_fmaf(hb, hb, -(a * c));
-        // sqrt_d without its branch: disc > 0 gives the same value; disc = +0
-        // gives 0 * inf = NaN inside the Newton steps and fmax(NaN, 0) = 0 =
-        // sqrt_d(0); disc < 0 is rejected below whatever sq is
-        const float sq = __builtin_fmaxf(disc * rsqrt_d(disc), 0.0f);
+        // disc < 0 is rejected below whatever sq is: no clamp
+        const float sq = sqrt_gs(disc);
         const bool neg = hb < 0.0f;
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
@@ -213,11 +210,10 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
         const bool win = !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
         bn = win ? num : bn;
         bq = win ? den : bq;
-        id = win ? i : id;
+        best = win ? r : best;
     };
     // scan order: axis-anchored walls (x, y, z), general huge spheres, small
-    // spheres; the winner's scan position indexes the shading records, which
-    // the host stores in the same order
+    // spheres (host: prepare_scan_order)
     int i = 0;
     for (; i < A.end_ax[0]; ++i)
         test(i, std::integral_constant<int, kAxX>{});
@@ -229,8 +225,8 @@ __device__ __forceinline__ int scene_scan(const KArgs &A, const GeoRec *geo, f3 
         test(i, std::integral_constant<int, kBig>{});
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
-    tbest = id >= 0 ? bn / bq : kInf;
-    return id;
+    tbest = best != recs + A.n ? bn / bq : kInf;
+    return best;
 }
 
 // Scenes with more than kLinearMax spheres: the huge
@@ -266,7 +262,7 @@ __device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1
     float disc = __builtin_fmaf(hb, hb, -(a * c));
     if (disc < 0.0f)
         return;
-    float sq = sqrt_d(disc);
+    float sq = sqrt_gs(disc);  // disc >= 0 here
     float num, den;
     if (hb < 0.0f) {
         float q = sq - hb;
@@ -343,16 +339,19 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
 template <bool kBvh, bool kCount = false>
-__device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const ShadeRec *shade, const float2 *trig,
-                                        f3 &o, f3 &d, f3 &T, f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
+__device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, const float2 *trig, f3 &o, f3 &d, f3 &T,
+                                        f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
 {
     float t;
-    int id;
-    if constexpr (kBvh)
-        id = scene_scan_bvh<kCount>(A, o, d, t, cnt);
-    else
-        id = scene_scan(A, geo, o, d, t);
-    if (id < 0) {  // main.cpp:115-120: sky
+    const ShadeRec *hit;
+    if constexpr (kBvh) {
+        const int id = scene_scan_bvh<kCount>(A, o, d, t, cnt);
+        hit = id >= 0 ? A.shade + id : nullptr;
+    } else {
+        const LinRec *w = scene_scan(A, recs, o, d, t);
+        hit = w != recs + A.n ? &w->s : nullptr;
+    }
+    if (!hit) {  // main.cpp:115-120: sky
         f3 ud = norm3(d);
         float tt = 0.5f * (ud.y + 1.0f);
         float it = 1.0f - tt;
@@ -361,7 +360,7 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const
                 __builtin_fmaf(T.z, __builtin_fmaf(tt, 1.0f, it), E.z));
         return true;
     }
-    const ShadeRec &S = shade[id];
+    const ShadeRec &S = *hit;
     float4 s0 = S.s0, s1 = S.s1;
     // hit_record.cpp:3-12
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
@@ -418,7 +417,7 @@ __device__ __forceinline__ bool segment(const KArgs &A, const GeoRec *geo, const
     // op3: diffuse -> cos theta = sqrt(1 - r); dielectric -> |r_out_parallel| (main.cpp:94)
     const f3 perp = mk3(__builtin_fmaf(nn.x, cthG, v1.x) * ratio, __builtin_fmaf(nn.y, cthG, v1.y) * ratio,
                         __builtin_fmaf(nn.z, cthG, v1.z) * ratio);
-    const float s3 = sqrt_d(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));
+    const float s3 = sqrt_gs(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));  // both >= 0
     f3 nd;
     if (isD) {  // main.cpp:53-55 (unit by construction, not re-normalised)
         f3 vv = cross3(nn, v1);
@@ -485,21 +484,16 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     // dynamic LDS: n geometry records then n shading records (96 B/sphere),
     // sized at launch so small scenes keep 8 workgroups per CU
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
-    GeoRec *lds_geo = reinterpret_cast<GeoRec *>(dyn_lds);
-    ShadeRec *lds_shade = reinterpret_cast<ShadeRec *>(dyn_lds + (size_t)A.n * sizeof(GeoRec));
-    const GeoRec *geo = A.geo;
-    const ShadeRec *shade = A.shade;
+    LinRec *lds_lin = reinterpret_cast<LinRec *>(dyn_lds);
+    const LinRec *recs = A.lin;
     __shared__ float2 lds_trig[kTrigEntries];
     static_assert(kTrigEntries <= kBlock, "one table entry per thread");
     if (threadIdx.x < kTrigEntries)
         lds_trig[threadIdx.x] = A.trig[threadIdx.x];
     if constexpr (kLdsGeo) {
-        for (int i = threadIdx.x; i < A.n; i += kBlock) {
-            lds_geo[i] = A.geo[i];
-            lds_shade[i] = A.shade[i];
-        }
-        geo = lds_geo;
-        shade = lds_shade;
+        for (int i = threadIdx.x; i <= A.n; i += kBlock)  // n records + the sentinel
+            lds_lin[i] = A.lin[i];
+        recs = lds_lin;
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -604,7 +598,6 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         atomicAdd(&lds_acc[wv][sl + 64], quant(ey));
         atomicAdd(&lds_acc[wv][sl + 128], quant(ez));
     };
-#if PTG_PARK_LDS
     // A finished path parks its radiance (E, slot) in the lane's LDS record
     // lds_pre[wv][lane], which just gave up its prefetched ray; the quantise +
     // LDS adds run for all parked lanes at the next refill batch (before the
@@ -627,7 +620,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         if (item >= 0) {
             if constexpr (kCount)
                 segs += 1;
-            if (segment<kBvh, kCount>(A, geo, shade, lds_trig, o, d, T, E, depth, st, scnt)) {
+            if (segment<kBvh, kCount>(A, recs, lds_trig, o, d, T, E, depth, st, scnt)) {
                 item = -1;
                 if (has_pre) {
                     const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
@@ -673,75 +666,6 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     }
     if (parked)
         flush_parked();
-#else
-    // A finished path parks its radiance in registers (pe, pslot); the
-    // quantise + LDS adds run for all parked lanes at the next refill batch,
-    // not in every iteration in which some lane finishes.  A lane parks at
-    // most one path: it finishes a second one only after using its prefetched
-    // ray, and then it waits, which forces a batch.
-    float pe_x = 0.0f, pe_y = 0.0f, pe_z = 0.0f;
-    int pslot = -1;
-    for (;;) {
-        if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
-            break;
-        if (item >= 0) {
-            if constexpr (kCount)
-                segs += 1;
-            if (segment<kBvh, kCount>(A, geo, shade, lds_trig, o, d, T, E, depth, st, scnt)) {
-                item = -1;
-                if (has_pre) {
-                    pe_x = E.x;
-                    pe_y = E.y;
-                    pe_z = E.z;
-                    pslot = slot;
-                    const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
-                    begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x),
-                          __float_as_uint(p1.y));
-                    has_pre = false;
-                } else {
-                    waiting = true;  // E is kept until the batch
-                }
-            }
-        }
-        if (next < total) {
-            const unsigned long long need = __ballot(!has_pre);
-            const int nn = (int)__popcll(need);
-            if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
-                const bool idle = waiting || item < 0;
-                if (pslot >= 0)
-                    flush(pe_x, pe_y, pe_z, pslot);
-                pslot = -1;
-                if (waiting) {
-                    pe_x = E.x;
-                    pe_y = E.y;
-                    pe_z = E.z;
-                    pslot = slot;
-                }
-                waiting = false;
-                if (!has_pre) {
-                    const int ni = next + (int)__popcll(need & ((1ull << lane) - 1ull));
-                    if (ni < total) {
-                        f3 ro, rd;
-                        uint32_t rs;
-                        ray_of(ni, ro, rd, rs);
-                        if (idle) {  // idle lane: start it now
-                            begin(ni, ro, rd, rs);
-                        } else {
-                            store_pre(ni, ro, rd, rs);
-                            has_pre = true;
-                        }
-                    }
-                }
-                next += nn;
-            }
-        } else if (waiting) {  // pool exhausted: nothing left for this lane
-            flush(E.x, E.y, E.z, slot);
-            waiting = false;
-        }
-    }
-    if (pslot >= 0)
-        flush(pe_x, pe_y, pe_z, pslot);
-#endif
     if constexpr (kCount) {
         unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes;
         for (int off = 32; off > 0; off >>= 1) {
@@ -846,7 +770,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *c
     while (!done) {
         segs += 1;
         ScanCount scnt;
-        done = segment<kBvh>(A, A.geo, A.shade, A.trig, o, d, T, E, depth, st, scnt);
+        done = segment<kBvh>(A, A.lin, A.trig, o, d, T, E, depth, st, scnt);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
@@ -884,8 +808,8 @@ __global__ void tonemap_kernel(const float *__restrict__ in, uint8_t *__restrict
 struct ptg_context {
     int device;
     int n;
-    GeoRec *d_geo;
-    ShadeRec *d_shade;
+    LinRec *d_lin;      // linear scenes
+    ShadeRec *d_shade;  // BVH scenes
     void *d_bvh;  // one allocation: nodes | leaf geometry | leaf ids | big geometry | big ids
     float2 *d_trig;  // sin/cos table (trig_table)
     unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
@@ -1189,24 +1113,27 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     prepare_scene(spheres, (int)n_spheres, cam, geo, shade, axis);
     KArgs order{};
     const bool linear = (int)n_spheres <= kLinearMax;
-    if (linear)  // the scan's record order; BVH scenes keep scene index order
+    std::vector<LinRec> lin;
+    if (linear) {  // the scan's record order, interleaved, + the no-hit sentinel
         prepare_scan_order(spheres, (int)n_spheres, geo, shade, axis, lgeo, lshade, order);
-    const std::vector<GeoRec> &up_geo = linear ? lgeo : geo;
-    const std::vector<ShadeRec> &up_shade = linear ? lshade : shade;
+        lin.resize(n_spheres + 1);
+        std::memset(lin.data(), 0, lin.size() * sizeof(LinRec));
+        for (size_t i = 0; i < n_spheres; ++i)
+            lin[i] = LinRec{lgeo[i], lshade[i]};
+    }
     ptg_context *ctx = new ptg_context();
     ctx->device = dev;
     ctx->n = (int)n_spheres;
-    size_t ng = std::max<size_t>(n_spheres, 1);
-    if (hipMalloc(&ctx->d_geo, ng * sizeof(GeoRec)) != hipSuccess ||
-        hipMalloc(&ctx->d_shade, ng * sizeof(ShadeRec)) != hipSuccess) {
-        (void)hipFree(ctx->d_geo);
+    // linear scenes: d_lin; BVH scenes: d_shade (scene index order) + d_bvh
+    const size_t bytes = linear ? lin.size() * sizeof(LinRec) : std::max<size_t>(n_spheres, 1) * sizeof(ShadeRec);
+    if (hipMalloc(linear ? (void **)&ctx->d_lin : (void **)&ctx->d_shade, bytes) != hipSuccess) {
         delete ctx;
         return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the scene failed");
     }
-    if (n_spheres) {
-        PTG_HIP(hipMemcpy(ctx->d_geo, up_geo.data(), n_spheres * sizeof(GeoRec), hipMemcpyHostToDevice));
-        PTG_HIP(hipMemcpy(ctx->d_shade, up_shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
-    }
+    if (linear)
+        PTG_HIP(hipMemcpy(ctx->d_lin, lin.data(), bytes, hipMemcpyHostToDevice));
+    else if (n_spheres)
+        PTG_HIP(hipMemcpy(ctx->d_shade, shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
     {
         float tab[2 * kTrigEntries];
         trig_table(tab);
@@ -1219,7 +1146,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     KArgs &A = ctx->base;
     std::memset(&A, 0, sizeof(A));
     A.trig = ctx->d_trig;
-    A.geo = ctx->d_geo;
+    A.lin = ctx->d_lin;
     A.shade = ctx->d_shade;
     A.n = (int)n_spheres;
     for (int k = 0; k < 3; ++k)
@@ -1302,8 +1229,10 @@ int ptg_context_destroy(ptg_context *ctx)
     if (!ctx)
         return PTG_OK;
     (void)hipSetDevice(ctx->device);
-    (void)hipFree(ctx->d_geo);
-    (void)hipFree(ctx->d_shade);
+    if (ctx->d_lin)
+        (void)hipFree(ctx->d_lin);
+    if (ctx->d_shade)
+        (void)hipFree(ctx->d_shade);
     if (ctx->d_trig)
         (void)hipFree(ctx->d_trig);
     if (ctx->d_bvh)
@@ -1342,7 +1271,7 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     if (grid <= 0)
         return PTG_OK;
     const bool bvh = A.n > kLinearMax;
-    const size_t lds = bvh ? 0 : (size_t)A.n * (sizeof(GeoRec) + sizeof(ShadeRec));
+    const size_t lds = bvh ? 0 : (size_t)(A.n + 1) * sizeof(LinRec);
     if (count)
         bvh ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, lds, s>>>(A);
     else

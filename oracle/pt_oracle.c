@@ -545,12 +545,26 @@ static float rsqrt_B(float x)
     t = fmaf(-h, t, 1.5f);
     return y * t;
 }
-/* sqrt(x) = x * rsqrt(x); 0 for x <= 0 */
-static float sqrt_B(float x) { return x > 0.0f ? x * rsqrt_B(x) : 0.0f; }
-/* the linear scan's branch-free form: fmax(x * rsqrt(x), 0).  Equal to
- * sqrt_B for x > 0 except subnormal x (-inf there -> 0); x = +0 gives
- * 0 * inf = NaN inside the Newton steps, and fmax(NaN, 0) = 0 */
-static float sqrt_scan_B(float x) { return fmaxf(x * rsqrt_B(x), 0.0f); }
+/* Deterministic square root for x >= 0 (x = +0 gives 0): the rsqrt_B seed,
+ * then two coupled Goldschmidt steps on g ~ sqrt(x), h ~ 1/(2 sqrt(x)).
+ * Kernel: pt_device.hpp sqrt_gs. */
+static float sqrt_gs_B(float x)
+{
+    uint32_t i;
+    memcpy(&i, &x, 4);
+    i = 0x5f375a86u - (i >> 1);
+    float y;
+    memcpy(&y, &i, 4);
+    float g = x * y;
+    float h = 0.5f * y;
+    float r = fmaf(-g, h, 0.5f);
+    g = fmaf(g, r, g);
+    h = fmaf(h, r, h);
+    r = fmaf(-g, h, 0.5f);
+    return fmaf(g, r, g);
+}
+/* sqrt for any x: 0 for x <= 0 */
+static float sqrt_B(float x) { return sqrt_gs_B(fmaxf(x, 0.0f)); }
 static f3 fnorm(f3 a)
 {
     float inv = rsqrt_B(fdot(a, a));
@@ -790,7 +804,7 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
         float disc = fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
-        float sq = sqrt_scan_B(disc);
+        float sq = sqrt_gs_B(disc); /* disc >= 0 here */
         float num, den;
         if (hb < 0.0f) {
             float q = sq - hb; /* > 0; roots c/q (near) and q/a (far) */
@@ -850,7 +864,7 @@ static int intersect_B_lex(const sphB *s, int n, f3 o, f3 d, float *tout, int *i
         float disc = fmaf(hb, hb, -(a * c));
         if (disc < 0.0f)
             continue;
-        float sq = sqrt_B(disc);
+        float sq = sqrt_gs_B(disc);
         float num, den;
         if (hb < 0.0f) {
             float q = sq - hb;
