@@ -55,8 +55,21 @@ __device__ __forceinline__ float sqrt_gs(float x)
     r = __builtin_fmaf(-g, h, 0.5f);
     return __builtin_fmaf(g, r, g);
 }
-// sqrt for any x: 0 for x <= 0
-__device__ __forceinline__ float sqrt_d(float x) { return sqrt_gs(__builtin_fmaxf(x, 0.0f)); }
+// sqrt for any x: 0 for x <= 0 (the clamp as an integer max: negative floats
+// are negative integers; one VALU, no canonicalisation)
+__device__ __forceinline__ float sqrt_d(float x) { return sqrt_gs(__int_as_float(max(__float_as_int(x), 0))); }
+// Deterministic n / d for d > 0 (normal): bit-trick reciprocal seed, two
+// Newton steps (error ~2e-4), then one residual correction of the quotient
+// (error ~1 ulp) -- 8 VALU instead of the IEEE division's 10 with a
+// transcendental.  The oracle's div_B executes the same operations.
+__device__ __forceinline__ float div_d(float n, float d)
+{
+    float r = __uint_as_float(0x7EF311C3u - __float_as_uint(d));
+    r = __builtin_fmaf(r, __builtin_fmaf(-d, r, 1.0f), r);
+    r = __builtin_fmaf(r, __builtin_fmaf(-d, r, 1.0f), r);
+    const float t = n * r;
+    return __builtin_fmaf(__builtin_fmaf(-d, t, n), r, t);
+}
 // vec.cpp:35-38: x * (1 / sqrt(x.x))
 __device__ __forceinline__ f3 norm3(f3 a)
 {

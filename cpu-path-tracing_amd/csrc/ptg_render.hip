@@ -225,7 +225,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         test(i, std::integral_constant<int, kBig>{});
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
-    tbest = best != recs + A.n ? bn / bq : kInf;
+    tbest = best != recs + A.n ? div_d(bn, bq) : kInf;
     return best;
 }
 

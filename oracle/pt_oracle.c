@@ -563,8 +563,29 @@ static float sqrt_gs_B(float x)
     r = fmaf(-g, h, 0.5f);
     return fmaf(g, r, g);
 }
-/* sqrt for any x: 0 for x <= 0 */
-static float sqrt_B(float x) { return sqrt_gs_B(fmaxf(x, 0.0f)); }
+/* sqrt for any x: 0 for x <= 0 (clamped as an integer max, like the kernel) */
+static float sqrt_B(float x)
+{
+    int32_t i;
+    memcpy(&i, &x, 4);
+    i = i > 0 ? i : 0;
+    memcpy(&x, &i, 4);
+    return sqrt_gs_B(x);
+}
+/* Deterministic n / d for d > 0: bit-trick reciprocal seed, two Newton steps,
+ * one residual correction of the quotient.  Kernel: pt_device.hpp div_d. */
+static float div_B(float n, float d)
+{
+    uint32_t i;
+    memcpy(&i, &d, 4);
+    i = 0x7EF311C3u - i;
+    float r;
+    memcpy(&r, &i, 4);
+    r = fmaf(r, fmaf(-d, r, 1.0f), r);
+    r = fmaf(r, fmaf(-d, r, 1.0f), r);
+    float t = n * r;
+    return fmaf(fmaf(-d, t, n), r, t);
+}
 static f3 fnorm(f3 a)
 {
     float inv = rsqrt_B(fdot(a, a));
@@ -829,7 +850,7 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
             id = i;
         }
     }
-    *tout = id >= 0 ? bn / bq : INFF;
+    *tout = id >= 0 ? div_B(bn, bq) : INFF;
     *idout = id;
     return id >= 0;
 }
@@ -1072,6 +1093,14 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
     if (segments)
         *segments = total;
     return 0;
+}
+
+void po_mode_b_math(const float *a, const float *b, size_t n, float *quot, float *root)
+{
+    for (size_t i = 0; i < n; ++i) {
+        quot[i] = div_B(a[i], b[i]);
+        root[i] = sqrt_B(a[i]);
+    }
 }
 
 void po_sincos2pi(const uint32_t *m, size_t n, float *out)

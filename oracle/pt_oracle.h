@@ -140,6 +140,9 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
                      uint64_t *segments);
 /* One Mode-B path for a given (pixel, sub, sample): returns radiance and
  * segment count -- used by the per-sample GPU parity test. */
+/* Mode B arithmetic primitives: quot[i] = div_B(a[i], b[i]) (b > 0),
+ * root[i] = sqrt_B(a[i]) */
+void po_mode_b_math(const float *a, const float *b, size_t n, float *quot, float *root);
 /* Mode B cos/sin(2 pi m 2^-24) of 24-bit integers m (out: n {cos, sin} pairs) */
 void po_sincos2pi(const uint32_t *m, size_t n, float *out);
 /* Mode B scene layout: anchor axis per sphere (-1: camera-facing anchor or not

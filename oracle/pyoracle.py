@@ -74,6 +74,7 @@ def lib():
             "po_tonemap": (None, [P, C.c_size_t, P]),
             "po_scan_layout": (I, [P, I, P, P, P]),
             "po_sincos2pi": (None, [P, C.c_size_t, P]),
+            "po_mode_b_math": (None, [P, P, C.c_size_t, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -215,3 +216,13 @@ def sincos2pi(m):
     out = np.zeros((m.size, 2), dtype=np.float32)
     lib().po_sincos2pi(ptr(m), m.size, ptr(out))
     return out
+
+
+def mode_b_math(a, b):
+    """Mode B division a / b (b > 0) and square root of a."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    q = np.zeros_like(a)
+    r = np.zeros_like(a)
+    lib().po_mode_b_math(ptr(a), ptr(b), a.size, ptr(q), ptr(r))
+    return q, r
