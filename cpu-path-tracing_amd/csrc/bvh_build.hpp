@@ -31,7 +31,10 @@ struct BvhNodeHost {
 };
 static_assert(sizeof(BvhNodeHost) == 32, "BVH node is two float4");
 
-constexpr int kLeafSize = 4;
+#ifndef PTG_BVH_LEAF
+#define PTG_BVH_LEAF 8  // measured on the 10,000-sphere scene: 8 beats 4 (-3.6 %) and 16 (+8.8 %)
+#endif
+constexpr int kLeafSize = PTG_BVH_LEAF;
 
 struct BvhBuild {
     std::vector<BvhNodeHost> nodes;

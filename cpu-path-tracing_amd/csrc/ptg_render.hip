@@ -70,6 +70,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_REFILL_BATCH
 #define PTG_REFILL_BATCH 32  // measured: 32 beats 16 and ties 48 (DESIGN.md perf log)
 #endif
+#ifndef PTG_LEAF_FRAC
+#define PTG_LEAF_FRAC 4  // BVH: leaf phase once half (4/8) of the unfinished lanes hold a leaf (8: all; 0: test leaves in place)
+#endif
+#ifndef PTG_WAVE_STATS
+#define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -303,6 +309,75 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     const float iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
     const float iz = d.z != 0.0f ? __builtin_amdgcn_rcpf(d.z) : __builtin_copysignf(1e30f, d.z);
     const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
+#if PTG_LEAF_FRAC
+    // "while-while" traversal (Aila & Laine 2009): a lane that reaches a leaf
+    // whose box its ray hits parks it (pend) and stops; the wave keeps
+    // walking inner nodes for the other lanes until enough lanes hold a leaf
+    // (PTG_LEAF_FRAC/8 of the lanes still walking or holding one), then every
+    // holding lane tests its own leaf's spheres at once.  Testing one lane's
+    // leaf at a time cost the whole wave ~4 sphere tests per visited leaf
+    // (SIMD efficiency of the leaf tests ~6 %).  The nearest-hit rule does not
+    // depend on the visiting order, so the result is the same bit for bit.
+    int ni = 0;
+    int pend = -1;  // parked leaf: first | count << 24
+    for (;;) {
+        for (;;) {
+            const bool walk = pend < 0 && ni < A.n_nodes;
+            const unsigned long long mw = __ballot(walk);
+            if (mw == 0ull)
+                break;
+            const int held = (int)__popcll(__ballot(pend >= 0));
+            if (8 * held >= PTG_LEAF_FRAC * (held + (int)__popcll(mw)))
+                break;
+#if PTG_WAVE_STATS  // debug: count wave-level node steps (first active lane only)
+            if constexpr (kCount)
+                cnt.boxes += (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ? 1 : 0;
+#endif
+            if (walk) {
+                const float4 n0 = A.bvh_nodes[2 * ni];
+                const float4 n1 = A.bvh_nodes[2 * ni + 1];
+#if !PTG_WAVE_STATS
+                if constexpr (kCount)
+                    cnt.boxes += 1;
+#endif
+                float tx1 = __builtin_fmaf(n0.x, ix, -ox), tx2 = __builtin_fmaf(n1.x, ix, -ox);
+                float ty1 = __builtin_fmaf(n0.y, iy, -oy), ty2 = __builtin_fmaf(n1.y, iy, -oy);
+                float tz1 = __builtin_fmaf(n0.z, iz, -oz), tz2 = __builtin_fmaf(n1.z, iz, -oz);
+                float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
+                                             __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
+                float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
+                                              __builtin_fminf(__builtin_fmaxf(tz1, tz2), tb * 1.0001f));
+                // selects, not branches: both words come with the node's two
+                // 16-B loads (a branch made the compiler fetch them later, one
+                // more dependent memory round trip per node)
+                const bool hit = !(t_in > t_out * 1.0001f + 1e-6f);
+                pend = hit ? __float_as_int(n1.w) : -1;  // -1 for inner nodes
+                ni = hit ? ni + 1 : __float_as_int(n0.w);  // miss: skip the subtree
+            }
+        }
+#if PTG_WAVE_STATS  // debug: wave-level leaf sphere-test iterations (max leaf size of the holding lanes)
+        if constexpr (kCount) {
+            int mx = pend >= 0 ? (pend >> 24) : 0;
+            for (int off = 32; off > 0; off >>= 1)
+                mx = max(mx, __shfl_xor(mx, off, 64));
+            cnt.spheres += (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ? mx : 0;
+        }
+#endif
+        if (pend >= 0) {
+            const int first = pend & 0xFFFFFF, nl = pend >> 24;
+#if !PTG_WAVE_STATS
+            if constexpr (kCount)
+                cnt.spheres += nl;
+#endif
+            for (int j = 0; j < nl; ++j)
+                test_sphere_lex<false>(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d,
+                                       a, tb, id);
+            pend = -1;
+        }
+        if (__ballot(ni < A.n_nodes) == 0ull)
+            break;
+    }
+#else
     int ni = 0;
     while (ni < A.n_nodes) {
         const float4 n0 = A.bvh_nodes[2 * ni];
@@ -331,6 +406,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
         }
         ++ni;
     }
+#endif
     tbest = tb;
     return id;
 }
