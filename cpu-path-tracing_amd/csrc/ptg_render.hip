@@ -73,6 +73,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_FRAC
 #define PTG_LEAF_FRAC 4  // BVH: leaf phase once half (4/8) of the unfinished lanes hold a leaf (8: all; 0: test leaves in place)
 #endif
+#ifndef PTG_READY_FRAC
+#define PTG_READY_FRAC 4  // BVH: stop walking and shade once 4/8 of the active lanes have finished their scan
+#endif
 #ifndef PTG_WAVE_STATS
 #define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
 #endif
@@ -411,9 +414,92 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     return id;
 }
 
+// Resumable BVH traversal (render kernel, scenes > kLinearMax): the state of
+// one lane's scan survives across iterations of the kernel's main loop, so
+// lanes whose scan ends early shade and start their next segment while the
+// wave keeps walking for the long rays (a wave otherwise waits for its
+// slowest ray: measured 93 wave-level node steps for 33 per ray on the
+// 10,000-sphere scene).
+struct BvhTrav {
+    int ni;    // next node in depth-first order (>= n_nodes: walk finished)
+    int pend;  // parked leaf (first | count << 24) or -1
+    float tb;  // nearest root so far
+    int id;    // its sphere (scene index) or -1
+};
+
+template <bool kCount>
+__device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
+{
+    const float a = dot3(d, d);
+    tr.tb = kInf;
+    tr.id = -1;
+    for (int k = 0; k < A.n_big; ++k)
+        test_sphere_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tr.tb, tr.id);
+    if constexpr (kCount)
+        cnt.spheres += A.n_big;
+    tr.ni = 0;
+    tr.pend = -1;
+}
+
+// Slab-test constants of a ray (culling only: fast reciprocals, padded boxes).
+struct SlabRay {
+    float ix, iy, iz, ox, oy, oz;
+};
+__device__ __forceinline__ SlabRay slab_ray(f3 o, f3 d)
+{
+    SlabRay r;
+    r.ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
+    r.iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
+    r.iz = d.z != 0.0f ? __builtin_amdgcn_rcpf(d.z) : __builtin_copysignf(1e30f, d.z);
+    r.ox = o.x * r.ix;
+    r.oy = o.y * r.iy;
+    r.oz = o.z * r.iz;
+    return r;
+}
+
+// One node step: test node tr.ni's box; hit -> descend (ni + 1; a leaf is
+// parked in tr.pend), miss -> skip the subtree.
+template <bool kCount>
+__device__ __forceinline__ void bvh_node_step(const KArgs &A, const SlabRay &r, BvhTrav &tr, ScanCount &cnt)
+{
+    const float4 n0 = A.bvh_nodes[2 * tr.ni];
+    const float4 n1 = A.bvh_nodes[2 * tr.ni + 1];
+    if constexpr (kCount)
+        cnt.boxes += 1;
+    const float tx1 = __builtin_fmaf(n0.x, r.ix, -r.ox), tx2 = __builtin_fmaf(n1.x, r.ix, -r.ox);
+    const float ty1 = __builtin_fmaf(n0.y, r.iy, -r.oy), ty2 = __builtin_fmaf(n1.y, r.iy, -r.oy);
+    const float tz1 = __builtin_fmaf(n0.z, r.iz, -r.oz), tz2 = __builtin_fmaf(n1.z, r.iz, -r.oz);
+    const float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
+                                       __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
+    const float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
+                                        __builtin_fminf(__builtin_fmaxf(tz1, tz2), tr.tb * 1.0001f));
+    const bool hit = !(t_in > t_out * 1.0001f + 1e-6f);
+    tr.pend = hit ? __float_as_int(n1.w) : -1;      // -1 for inner nodes
+    tr.ni = hit ? tr.ni + 1 : __float_as_int(n0.w);  // miss: skip the subtree
+}
+
+// The parked leaf's spheres (the reference's nearest-hit rule).
+template <bool kCount>
+__device__ __forceinline__ void bvh_leaf(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
+{
+    const float a = dot3(d, d);
+    const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
+    if constexpr (kCount)
+        cnt.spheres += nl;
+    for (int j = 0; j < nl; ++j)
+        test_sphere_lex<false>(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d, a,
+                               tr.tb, tr.id);
+    tr.pend = -1;
+}
+
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
+// shade(): everything after the scene scan -- sky on a miss, else hit
+// record, emission, Russian roulette, BRDF sampling of the next ray.
+__device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
+                                      int &depth, uint32_t &st);
+
 template <bool kBvh, bool kCount = false>
 __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, const float2 *trig, f3 &o, f3 &d, f3 &T,
                                         f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
@@ -427,6 +513,12 @@ __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, cons
         const LinRec *w = scene_scan(A, recs, o, d, t);
         hit = w != recs + A.n ? &w->s : nullptr;
     }
+    return shade(hit, t, trig, o, d, T, E, depth, st);
+}
+
+__device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
+                                      int &depth, uint32_t &st)
+{
     if (!hit) {  // main.cpp:115-120: sky
         f3 ud = norm3(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -639,8 +731,10 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         L.key = lds_key[wv][sl];
         camera_ray(A, L, (uint32_t)sample, rs, ro, rd);
     };
+    int phase = 0;  // BVH scenes: 0 fresh ray, 1 walking, 2 scan done (resumable scan, see below)
     auto begin = [&](int it, f3 ro, f3 rd, uint32_t rs) {
         item = it;
+        phase = 0;
         slot = nv == 64 ? (it & 63) : it % nv;
         o = ro;
         d = rd;
@@ -690,25 +784,21 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         flush(pk.x, pk.y, pk.z, __float_as_int(pk.w));
         parked = false;
     };
-    for (;;) {
-        if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
-            break;
-        if (item >= 0) {
-            if constexpr (kCount)
-                segs += 1;
-            if (segment<kBvh, kCount>(A, recs, lds_trig, o, d, T, E, depth, st, scnt)) {
-                item = -1;
-                if (has_pre) {
-                    const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
-                    park();
-                    begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x),
-                          __float_as_uint(p1.y));
-                    has_pre = false;
-                } else {
-                    waiting = true;  // E is kept until the batch
-                }
-            }
+    // path end: park the radiance and start the prefetched ray, or wait
+    auto path_done = [&]() {
+        item = -1;
+        if (has_pre) {
+            const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
+            park();
+            begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
+            has_pre = false;
+        } else {
+            waiting = true;  // E is kept until the batch
         }
+    };
+    // refill batch: flush parked paths, prefetch camera rays for lanes
+    // without one, start idle lanes
+    auto refill = [&]() {
         if (next < total) {
             const unsigned long long need = __ballot(!has_pre);
             const int nn = (int)__popcll(need);
@@ -738,6 +828,76 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         } else if (waiting) {  // pool exhausted: nothing left for this lane
             flush(E.x, E.y, E.z, slot);
             waiting = false;
+        }
+    };
+    if constexpr (!kBvh) {
+        for (;;) {
+            if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+                break;
+            if (item >= 0) {
+                if constexpr (kCount)
+                    segs += 1;
+                if (segment<kBvh, kCount>(A, recs, lds_trig, o, d, T, E, depth, st, scnt))
+                    path_done();
+            }
+            refill();
+        }
+    } else {
+        // BVH scenes: each lane is fresh (ray set, scan not started), walking
+        // or ready (scan done, to be shaded); an iteration starts the fresh
+        // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
+        // of the active lanes) or none walks, shades the ready lanes.
+        BvhTrav tr{0, -1, kInf, -1};
+        for (;;) {
+            if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+                break;
+            if (item >= 0 && phase == 0) {
+                if constexpr (kCount)
+                    segs += 1;
+                bvh_start<kCount>(A, o, d, tr, scnt);
+                phase = tr.ni < A.n_nodes ? 1 : 2;
+            }
+            {
+                const SlabRay sr = slab_ray(o, d);
+                for (;;) {
+                    const bool trv = item >= 0 && phase == 1;
+                    const unsigned long long mt = __ballot(trv);
+                    if (mt == 0ull)
+                        break;
+                    const int nt = (int)__popcll(mt);
+                    const int na = (int)__popcll(__ballot(item >= 0));
+                    if (8 * (na - nt) >= PTG_READY_FRAC * na)
+                        break;
+                    const int nh = (int)__popcll(__ballot(trv && tr.pend >= 0));
+#if PTG_WAVE_STATS  // debug: wave-level node steps / leaf sphere iterations (first active lane only)
+                    if constexpr (kCount) {
+                        const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
+                        if (8 * nh >= PTG_LEAF_FRAC * nt) {
+                            int mx = trv && tr.pend >= 0 ? (tr.pend >> 24) : 0;
+                            for (int off = 32; off > 0; off >>= 1)
+                                mx = max(mx, __shfl_xor(mx, off, 64));
+                            scnt.spheres += first_lane ? mx : 0;
+                        } else {
+                            scnt.boxes += first_lane ? 1 : 0;
+                        }
+                    }
+#endif
+                    if (8 * nh >= PTG_LEAF_FRAC * nt) {  // leaf phase
+                        if (trv && tr.pend >= 0)
+                            bvh_leaf<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt);
+                    } else if (trv && tr.pend < 0) {  // node step
+                        bvh_node_step<kCount && !PTG_WAVE_STATS>(A, sr, tr, scnt);
+                    }
+                    if (trv && tr.pend < 0 && tr.ni >= A.n_nodes)
+                        phase = 2;
+                }
+            }
+            if (item >= 0 && phase == 2) {
+                phase = 0;
+                if (shade(tr.id >= 0 ? A.shade + tr.id : nullptr, tr.tb, lds_trig, o, d, T, E, depth, st))
+                    path_done();
+            }
+            refill();
         }
     }
     if (parked)
