@@ -110,4 +110,47 @@ inline BvhBuild build_bvh(const ptg_sphere *s, int n, double big_radius)
     return b;
 }
 
+// Compact 16-B nodes: the box quantised to 16 bits per coordinate on the
+// root box's grid (rounded outward by one more step: conservative), and one
+// word: >= 0 inner node's skip index, < 0 leaf (INT_MIN | count << 24 | first;
+// a leaf's skip is the next node).  The kernel transforms the ray into grid
+// units once per ray (t = q * (scale / d) + (lo - o) / d), so a node costs
+// one 16-B load instead of two.
+struct BvhNodeQ {
+    uint32_t xy_min, z_min_x_max, y_max_z_max;
+    int32_t word;
+};
+static_assert(sizeof(BvhNodeQ) == 16, "compact BVH node is one float4");
+
+struct BvhGrid {
+    float lo[3], scale[3];
+};
+
+inline BvhGrid quantise_bvh(const std::vector<BvhNodeHost> &nodes, std::vector<BvhNodeQ> &out)
+{
+    BvhGrid g{};
+    out.resize(nodes.size());
+    if (nodes.empty())
+        return g;
+    double lo[3], sc[3];
+    for (int c = 0; c < 3; ++c) {
+        lo[c] = nodes[0].bmin[c];
+        const double ext = (double)nodes[0].bmax[c] - lo[c];
+        sc[c] = ext > 0.0 ? ext / 65533.0 : 1e-30;
+        g.lo[c] = (float)lo[c];
+        g.scale[c] = (float)sc[c];
+    }
+    auto qlo = [&](double v, int c) { return (uint32_t)std::clamp(std::floor((v - lo[c]) / sc[c]) - 1.0, 0.0, 65535.0); };
+    auto qhi = [&](double v, int c) { return (uint32_t)std::clamp(std::ceil((v - lo[c]) / sc[c]) + 1.0, 0.0, 65535.0); };
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const BvhNodeHost &n = nodes[i];
+        BvhNodeQ &q = out[i];
+        q.xy_min = qlo(n.bmin[0], 0) | (qlo(n.bmin[1], 1) << 16);
+        q.z_min_x_max = qlo(n.bmin[2], 2) | (qhi(n.bmax[0], 0) << 16);
+        q.y_max_z_max = qhi(n.bmax[1], 1) | (qhi(n.bmax[2], 2) << 16);
+        q.word = n.leaf >= 0 ? (int32_t)(0x80000000u | (uint32_t)n.leaf) : n.skip;
+    }
+    return g;
+}
+
 }  // namespace ptg

@@ -97,6 +97,8 @@ struct KArgs {
     int end_big;
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
+    const uint4 *bvh_qnodes;  // the same nodes, compact (bvh_build.hpp BvhNodeQ; render kernel)
+    float q_lo[3], q_scale[3];
     const GeoRec *bvh_geo;    // leaf-ordered geometry
     const int *bvh_id;        // leaf-ordered scene indices
     const GeoRec *big_geo;    // huge spheres, tested linearly
@@ -441,19 +443,24 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.pend = -1;
 }
 
-// Slab-test constants of a ray (culling only: fast reciprocals, padded boxes).
+// Slab-test constants of a ray in the compact nodes' grid units (culling
+// only: fast reciprocals, boxes padded and rounded outward):
+// t = q * (scale / d) + (lo - o) / d.
 struct SlabRay {
-    float ix, iy, iz, ox, oy, oz;
+    float sx, sy, sz, bx, by, bz;
 };
-__device__ __forceinline__ SlabRay slab_ray(f3 o, f3 d)
+__device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
 {
+    const float ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
+    const float iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
+    const float iz = d.z != 0.0f ? __builtin_amdgcn_rcpf(d.z) : __builtin_copysignf(1e30f, d.z);
     SlabRay r;
-    r.ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
-    r.iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
-    r.iz = d.z != 0.0f ? __builtin_amdgcn_rcpf(d.z) : __builtin_copysignf(1e30f, d.z);
-    r.ox = o.x * r.ix;
-    r.oy = o.y * r.iy;
-    r.oz = o.z * r.iz;
+    r.sx = A.q_scale[0] * ix;
+    r.sy = A.q_scale[1] * iy;
+    r.sz = A.q_scale[2] * iz;
+    r.bx = (A.q_lo[0] - o.x) * ix;
+    r.by = (A.q_lo[1] - o.y) * iy;
+    r.bz = (A.q_lo[2] - o.z) * iz;
     return r;
 }
 
@@ -462,20 +469,23 @@ __device__ __forceinline__ SlabRay slab_ray(f3 o, f3 d)
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(const KArgs &A, const SlabRay &r, BvhTrav &tr, ScanCount &cnt)
 {
-    const float4 n0 = A.bvh_nodes[2 * tr.ni];
-    const float4 n1 = A.bvh_nodes[2 * tr.ni + 1];
+    const uint4 q = A.bvh_qnodes[tr.ni];  // one 16-B load
     if constexpr (kCount)
         cnt.boxes += 1;
-    const float tx1 = __builtin_fmaf(n0.x, r.ix, -r.ox), tx2 = __builtin_fmaf(n1.x, r.ix, -r.ox);
-    const float ty1 = __builtin_fmaf(n0.y, r.iy, -r.oy), ty2 = __builtin_fmaf(n1.y, r.iy, -r.oy);
-    const float tz1 = __builtin_fmaf(n0.z, r.iz, -r.oz), tz2 = __builtin_fmaf(n1.z, r.iz, -r.oz);
+    const float tx1 = __builtin_fmaf((float)(q.x & 0xFFFFu), r.sx, r.bx);
+    const float ty1 = __builtin_fmaf((float)(q.x >> 16), r.sy, r.by);
+    const float tz1 = __builtin_fmaf((float)(q.y & 0xFFFFu), r.sz, r.bz);
+    const float tx2 = __builtin_fmaf((float)(q.y >> 16), r.sx, r.bx);
+    const float ty2 = __builtin_fmaf((float)(q.z & 0xFFFFu), r.sy, r.by);
+    const float tz2 = __builtin_fmaf((float)(q.z >> 16), r.sz, r.bz);
     const float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
                                        __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
     const float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
                                         __builtin_fminf(__builtin_fmaxf(tz1, tz2), tr.tb * 1.0001f));
     const bool hit = !(t_in > t_out * 1.0001f + 1e-6f);
-    tr.pend = hit ? __float_as_int(n1.w) : -1;      // -1 for inner nodes
-    tr.ni = hit ? tr.ni + 1 : __float_as_int(n0.w);  // miss: skip the subtree
+    const int w = (int)q.w;  // >= 0 inner node's skip; < 0 leaf (its skip is the next node)
+    tr.pend = (hit && w < 0) ? (w & 0x7FFFFFFF) : -1;
+    tr.ni = (hit || w < 0) ? tr.ni + 1 : w;
 }
 
 // The parked leaf's spheres (the reference's nearest-hit rule).
@@ -858,7 +868,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                 phase = tr.ni < A.n_nodes ? 1 : 2;
             }
             {
-                const SlabRay sr = slab_ray(o, d);
+                const SlabRay sr = slab_ray(A, o, d);
                 for (;;) {
                     const bool trv = item >= 0 && phase == 1;
                     const unsigned long long mt = __ballot(trv);
@@ -1390,14 +1400,22 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.end_big = order.end_big;
     if ((int)n_spheres > kLinearMax) {
         BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);
+        std::vector<BvhNodeQ> qn;
+        const BvhGrid grid = quantise_bvh(b.nodes, qn);
         const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();
         const size_t off_geo = n_nodes * sizeof(BvhNodeHost);
         const size_t off_id = off_geo + n_leaf * sizeof(GeoRec);
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
-        const size_t total = off_bid + n_big * sizeof(int) + 16;
+        const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
+        const size_t total = off_q + n_nodes * sizeof(BvhNodeQ) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
+        std::memcpy(blob.data() + off_q, qn.data(), n_nodes * sizeof(BvhNodeQ));
+        for (int c = 0; c < 3; ++c) {
+            A.q_lo[c] = grid.lo[c];
+            A.q_scale[c] = grid.scale[c];
+        }
         for (size_t i = 0; i < n_leaf; ++i) {
             std::memcpy(blob.data() + off_geo + i * sizeof(GeoRec), &geo[b.order[i]], sizeof(GeoRec));
             std::memcpy(blob.data() + off_id + i * sizeof(int), &b.order[i], sizeof(int));
@@ -1413,6 +1431,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         PTG_HIP(hipMemcpy(ctx->d_bvh, blob.data(), total, hipMemcpyHostToDevice));
         unsigned char *base = static_cast<unsigned char *>(ctx->d_bvh);
         A.bvh_nodes = reinterpret_cast<const float4 *>(base);
+        A.bvh_qnodes = reinterpret_cast<const uint4 *>(base + off_q);
         A.bvh_geo = reinterpret_cast<const GeoRec *>(base + off_geo);
         A.bvh_id = reinterpret_cast<const int *>(base + off_id);
         A.big_geo = reinterpret_cast<const GeoRec *>(base + off_bgeo);
