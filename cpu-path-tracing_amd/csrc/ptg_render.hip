@@ -71,7 +71,7 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #define PTG_REFILL_BATCH 32  // measured: 32 beats 16 and ties 48 (DESIGN.md perf log)
 #endif
 #ifndef PTG_LEAF_FRAC
-#define PTG_LEAF_FRAC 4  // BVH: leaf phase once half (4/8) of the unfinished lanes hold a leaf (8: all; 0: test leaves in place)
+#define PTG_LEAF_FRAC 4  // BVH: leaf phase once half (4/8) of the walking lanes hold a leaf (8: all)
 #endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 4  // BVH: stop walking and shade once 4/8 of the active lanes have finished their scan
@@ -99,7 +99,7 @@ struct KArgs {
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
     const uint4 *bvh_qnodes;  // the same nodes, compact (bvh_build.hpp BvhNodeQ; render kernel)
     float q_lo[3], q_scale[3];
-    const GeoRec *bvh_geo;    // leaf-ordered geometry
+    const float4 *bvh_sph;    // leaf-ordered spheres {C, -R^2} (BVH leaves hold only non-huge spheres)
     const int *bvh_id;        // leaf-ordered scene indices
     const GeoRec *big_geo;    // huge spheres, tested linearly
     const int *big_id;
@@ -251,28 +251,34 @@ struct ScanCount {
     uint32_t spheres = 0, boxes = 0;  // sphere tests and box tests of the BVH walk (counting kernel only)
 };
 
-template <bool kMaybeBig>  // BVH leaves hold only non-huge spheres (bvh_build.hpp)
-__device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1, const int gid, const f3 o,
-                                                const f3 d, const float a, float &tb, int &id)
+// Root of one sphere under the reference's rule (the root >= eps nearest to
+// the origin, t = fl(num/den)); NaN when rejected or provably not below tb
+// (the two exact culls of DESIGN.md "scene scan").  kBig: anchored form with
+// g0 = {P0, R}, g1 = {n0, 2R} (huge spheres); else g0 = {C, -R^2}.
+constexpr float kReject = __builtin_nanf("");  // every comparison with it is false
+
+template <bool kBig>
+__device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, const f3 o, const f3 d, const float a,
+                                          const float tb)
 {
     f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
     float ed = dot3(e, d);
     float ee = dot3(e, e);
     float hb, c;
-    if (kMaybeBig && g0.w >= 0.0f) {
+    if constexpr (kBig) {
         hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
         c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
     } else {
         hb = ed;
-        c = ee + g1.w;
+        c = ee + g0.w;
     }
     if (hb >= 0.0f && c >= 0.0f)
-        return;
+        return kReject;
     if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * kCullMargin)
-        return;  // near root > tb (exact, see scene_scan)
+        return kReject;  // near root > tb
     float disc = __builtin_fmaf(hb, hb, -(a * c));
     if (disc < 0.0f)
-        return;
+        return kReject;
     float sq = sqrt_gs(disc);  // disc >= 0 here
     float num, den;
     if (hb < 0.0f) {
@@ -283,160 +289,60 @@ __device__ __forceinline__ void test_sphere_lex(const float4 g0, const float4 g1
             num = q;
             den = a;
             if (q < kEps * a)
-                return;
+                return kReject;
         }
     } else {
         float qn = hb + sq;
         num = -c;
         den = qn;
         if (num < kEps * den)
-            return;
+            return kReject;
     }
-    const float t = num / den;
-    if (t < tb || (t == tb && gid < id)) {
-        tb = t;
-        id = gid;
-    }
+    return num / den;
 }
 
-template <bool kCount>
-__device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest, ScanCount &cnt)
+// The BVH scan's winner is encoded: -1 none, >= 0 a leaf-order index (its
+// scene index bvh_id[k] is read only on exact ties and for the final
+// winner), <= -2 the huge sphere with scene index -2 - best.  Ties of t go
+// to the lowest scene index (main.cpp:35: strict < in index order), which
+// makes the result independent of the visiting order: the oracle's linear
+// scan (intersect_B_lex) gives the same bits.
+__device__ __forceinline__ int scene_id_of(const KArgs &A, int best)
 {
-    const float a = dot3(d, d);
-    float tb = kInf;
-    int id = -1;
-    for (int k = 0; k < A.n_big; ++k)
-        test_sphere_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tb, id);
-    if constexpr (kCount)
-        cnt.spheres += A.n_big;
-    // slab test (culling only: fast reciprocals, padded boxes)
-    const float ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
-    const float iy = d.y != 0.0f ? __builtin_amdgcn_rcpf(d.y) : __builtin_copysignf(1e30f, d.y);
-    const float iz = d.z != 0.0f ? __builtin_amdgcn_rcpf(d.z) : __builtin_copysignf(1e30f, d.z);
-    const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
-#if PTG_LEAF_FRAC
-    // "while-while" traversal (Aila & Laine 2009): a lane that reaches a leaf
-    // whose box its ray hits parks it (pend) and stops; the wave keeps
-    // walking inner nodes for the other lanes until enough lanes hold a leaf
-    // (PTG_LEAF_FRAC/8 of the lanes still walking or holding one), then every
-    // holding lane tests its own leaf's spheres at once.  Testing one lane's
-    // leaf at a time cost the whole wave ~4 sphere tests per visited leaf
-    // (SIMD efficiency of the leaf tests ~6 %).  The nearest-hit rule does not
-    // depend on the visiting order, so the result is the same bit for bit.
-    int ni = 0;
-    int pend = -1;  // parked leaf: first | count << 24
-    for (;;) {
-        for (;;) {
-            const bool walk = pend < 0 && ni < A.n_nodes;
-            const unsigned long long mw = __ballot(walk);
-            if (mw == 0ull)
-                break;
-            const int held = (int)__popcll(__ballot(pend >= 0));
-            if (8 * held >= PTG_LEAF_FRAC * (held + (int)__popcll(mw)))
-                break;
-#if PTG_WAVE_STATS  // debug: count wave-level node steps (first active lane only)
-            if constexpr (kCount)
-                cnt.boxes += (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ? 1 : 0;
-#endif
-            if (walk) {
-                const float4 n0 = A.bvh_nodes[2 * ni];
-                const float4 n1 = A.bvh_nodes[2 * ni + 1];
-#if !PTG_WAVE_STATS
-                if constexpr (kCount)
-                    cnt.boxes += 1;
-#endif
-                float tx1 = __builtin_fmaf(n0.x, ix, -ox), tx2 = __builtin_fmaf(n1.x, ix, -ox);
-                float ty1 = __builtin_fmaf(n0.y, iy, -oy), ty2 = __builtin_fmaf(n1.y, iy, -oy);
-                float tz1 = __builtin_fmaf(n0.z, iz, -oz), tz2 = __builtin_fmaf(n1.z, iz, -oz);
-                float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
-                                             __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
-                float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
-                                              __builtin_fminf(__builtin_fmaxf(tz1, tz2), tb * 1.0001f));
-                // selects, not branches: both words come with the node's two
-                // 16-B loads (a branch made the compiler fetch them later, one
-                // more dependent memory round trip per node)
-                const bool hit = !(t_in > t_out * 1.0001f + 1e-6f);
-                pend = hit ? __float_as_int(n1.w) : -1;  // -1 for inner nodes
-                ni = hit ? ni + 1 : __float_as_int(n0.w);  // miss: skip the subtree
-            }
+    return best >= 0 ? A.bvh_id[best] : (best == -1 ? -1 : -2 - best);
+}
+__device__ __forceinline__ void update_lex(const KArgs &A, const float t, const int cand, float &tb, int &best)
+{
+    if (t <= tb) {  // NaN (rejected) fails; rarely taken
+        if (t < tb || scene_id_of(A, cand) < scene_id_of(A, best)) {  // nearer, or an exact tie with a lower index
+            tb = t;
+            best = cand;
         }
-#if PTG_WAVE_STATS  // debug: wave-level leaf sphere-test iterations (max leaf size of the holding lanes)
-        if constexpr (kCount) {
-            int mx = pend >= 0 ? (pend >> 24) : 0;
-            for (int off = 32; off > 0; off >>= 1)
-                mx = max(mx, __shfl_xor(mx, off, 64));
-            cnt.spheres += (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ? mx : 0;
-        }
-#endif
-        if (pend >= 0) {
-            const int first = pend & 0xFFFFFF, nl = pend >> 24;
-#if !PTG_WAVE_STATS
-            if constexpr (kCount)
-                cnt.spheres += nl;
-#endif
-            for (int j = 0; j < nl; ++j)
-                test_sphere_lex<false>(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d,
-                                       a, tb, id);
-            pend = -1;
-        }
-        if (__ballot(ni < A.n_nodes) == 0ull)
-            break;
     }
-#else
-    int ni = 0;
-    while (ni < A.n_nodes) {
-        const float4 n0 = A.bvh_nodes[2 * ni];
-        const float4 n1 = A.bvh_nodes[2 * ni + 1];
-        if constexpr (kCount)
-            cnt.boxes += 1;
-        float tx1 = __builtin_fmaf(n0.x, ix, -ox), tx2 = __builtin_fmaf(n1.x, ix, -ox);
-        float ty1 = __builtin_fmaf(n0.y, iy, -oy), ty2 = __builtin_fmaf(n1.y, iy, -oy);
-        float tz1 = __builtin_fmaf(n0.z, iz, -oz), tz2 = __builtin_fmaf(n1.z, iz, -oz);
-        float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
-                                     __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
-        float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
-                                      __builtin_fminf(__builtin_fmaxf(tz1, tz2), tb * 1.0001f));
-        if (t_in > t_out * 1.0001f + 1e-6f) {
-            ni = __float_as_int(n0.w);  // skip the subtree
-            continue;
-        }
-        const int leaf = __float_as_int(n1.w);
-        if (leaf >= 0) {
-            const int first = leaf & 0xFFFFFF, nl = leaf >> 24;
-            if constexpr (kCount)
-                cnt.spheres += nl;
-            for (int j = 0; j < nl; ++j)
-                test_sphere_lex<false>(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d,
-                                       a, tb, id);
-        }
-        ++ni;
-    }
-#endif
-    tbest = tb;
-    return id;
 }
 
-// Resumable BVH traversal (render kernel, scenes > kLinearMax): the state of
-// one lane's scan survives across iterations of the kernel's main loop, so
-// lanes whose scan ends early shade and start their next segment while the
-// wave keeps walking for the long rays (a wave otherwise waits for its
-// slowest ray: measured 93 wave-level node steps for 33 per ray on the
-// 10,000-sphere scene).
+// Per-lane BVH scan state.  The render kernel keeps it across iterations of
+// its main loop (resumable scan): lanes whose scan ends early shade and start
+// their next segment while the wave keeps walking for the long rays -- a
+// wave otherwise waits for its slowest ray (measured 93 wave-level node
+// steps for 33 per ray on the 10,000-sphere scene).
 struct BvhTrav {
     int ni;    // next node in depth-first order (>= n_nodes: walk finished)
     int pend;  // parked leaf (first | count << 24) or -1
     float tb;  // nearest root so far
-    int id;    // its sphere (scene index) or -1
+    int best;  // encoded winner (scene_id_of)
 };
 
+// Start a scan: the huge spheres (tested linearly, first), then the BVH.
 template <bool kCount>
 __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
     const float a = dot3(d, d);
     tr.tb = kInf;
-    tr.id = -1;
+    tr.best = -1;
     for (int k = 0; k < A.n_big; ++k)
-        test_sphere_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, A.big_id[k], o, d, a, tr.tb, tr.id);
+        update_lex(A, root_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), -2 - A.big_id[k], tr.tb,
+                   tr.best);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
     tr.ni = 0;
@@ -488,7 +394,7 @@ __device__ __forceinline__ void bvh_node_step(const KArgs &A, const SlabRay &r, 
     tr.ni = (hit || w < 0) ? tr.ni + 1 : w;
 }
 
-// The parked leaf's spheres (the reference's nearest-hit rule).
+// The parked leaf's spheres: compact records {C, -R^2} in leaf order.
 template <bool kCount>
 __device__ __forceinline__ void bvh_leaf(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
@@ -497,9 +403,25 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, f3 o, f3 d, BvhTrav &tr
     if constexpr (kCount)
         cnt.spheres += nl;
     for (int j = 0; j < nl; ++j)
-        test_sphere_lex<false>(A.bvh_geo[first + j].g0, A.bvh_geo[first + j].g1, A.bvh_id[first + j], o, d, a,
-                               tr.tb, tr.id);
+        update_lex(A, root_lex<false>(A.bvh_sph[first + j], float4{}, o, d, a, tr.tb), first + j, tr.tb, tr.best);
     tr.pend = -1;
+}
+
+// Whole scan of one ray (parity probe kernel): walk, testing each parked leaf
+// at once.
+template <bool kCount>
+__device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest, ScanCount &cnt)
+{
+    BvhTrav tr;
+    bvh_start<kCount>(A, o, d, tr, cnt);
+    const SlabRay sr = slab_ray(A, o, d);
+    while (tr.ni < A.n_nodes) {
+        bvh_node_step<kCount>(A, sr, tr, cnt);
+        if (tr.pend >= 0)
+            bvh_leaf<kCount>(A, o, d, tr, cnt);
+    }
+    tbest = tr.tb;
+    return scene_id_of(A, tr.best);
 }
 
 // Per-lane state machine: one call = one bounce segment of radiance()
@@ -857,7 +779,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
         // or ready (scan done, to be shaded); an iteration starts the fresh
         // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
         // of the active lanes) or none walks, shades the ready lanes.
-        BvhTrav tr{0, -1, kInf, -1};
+        BvhTrav tr{0, -1, kInf, -1};  // started per segment by bvh_start
         for (;;) {
             if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
                 break;
@@ -904,7 +826,8 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
             }
             if (item >= 0 && phase == 2) {
                 phase = 0;
-                if (shade(tr.id >= 0 ? A.shade + tr.id : nullptr, tr.tb, lds_trig, o, d, T, E, depth, st))
+                const int id = scene_id_of(A, tr.best);
+                if (shade(id >= 0 ? A.shade + id : nullptr, tr.tb, lds_trig, o, d, T, E, depth, st))
                     path_done();
             }
             refill();
@@ -1404,7 +1327,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const BvhGrid grid = quantise_bvh(b.nodes, qn);
         const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();
         const size_t off_geo = n_nodes * sizeof(BvhNodeHost);
-        const size_t off_id = off_geo + n_leaf * sizeof(GeoRec);
+        const size_t off_id = off_geo + n_leaf * sizeof(float4);
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
         const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
@@ -1417,7 +1340,10 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             A.q_scale[c] = grid.scale[c];
         }
         for (size_t i = 0; i < n_leaf; ++i) {
-            std::memcpy(blob.data() + off_geo + i * sizeof(GeoRec), &geo[b.order[i]], sizeof(GeoRec));
+            const ptg_sphere &sp = spheres[b.order[i]];  // leaf record {C, -R^2}, as the GeoRec of a small sphere
+            const float4 rec = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2],
+                                           (float)(-(sp.radius * sp.radius)));
+            std::memcpy(blob.data() + off_geo + i * sizeof(float4), &rec, sizeof(float4));
             std::memcpy(blob.data() + off_id + i * sizeof(int), &b.order[i], sizeof(int));
         }
         for (size_t i = 0; i < n_big; ++i) {
@@ -1432,7 +1358,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         unsigned char *base = static_cast<unsigned char *>(ctx->d_bvh);
         A.bvh_nodes = reinterpret_cast<const float4 *>(base);
         A.bvh_qnodes = reinterpret_cast<const uint4 *>(base + off_q);
-        A.bvh_geo = reinterpret_cast<const GeoRec *>(base + off_geo);
+        A.bvh_sph = reinterpret_cast<const float4 *>(base + off_geo);
         A.bvh_id = reinterpret_cast<const int *>(base + off_id);
         A.big_geo = reinterpret_cast<const GeoRec *>(base + off_bgeo);
         A.big_id = reinterpret_cast<const int *>(base + off_bid);
