@@ -301,23 +301,16 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
     return num / den;
 }
 
-// The BVH scan's winner is encoded: -1 none, >= 0 a leaf-order index (its
-// scene index bvh_id[k] is read only on exact ties and for the final
-// winner), <= -2 the huge sphere with scene index -2 - best.  Ties of t go
-// to the lowest scene index (main.cpp:35: strict < in index order), which
-// makes the result independent of the visiting order: the oracle's linear
-// scan (intersect_B_lex) gives the same bits.
-__device__ __forceinline__ int scene_id_of(const KArgs &A, int best)
+// The BVH scan's winner is its scene index (-1: none).  Ties of t go to the
+// lowest scene index (main.cpp:35: strict < in index order), which makes the
+// result independent of the visiting order: the oracle's linear scan
+// (intersect_B_lex) gives the same bits.
+__device__ __forceinline__ void update_lex(const float t, const int sid, float &tb, int &best)
 {
-    return best >= 0 ? A.bvh_id[best] : (best == -1 ? -1 : -2 - best);
-}
-__device__ __forceinline__ void update_lex(const KArgs &A, const float t, const int cand, float &tb, int &best)
-{
-    if (t <= tb) {  // NaN (rejected) fails; rarely taken
-        if (t < tb || scene_id_of(A, cand) < scene_id_of(A, best)) {  // nearer, or an exact tie with a lower index
-            tb = t;
-            best = cand;
-        }
+    // t <= tb: NaN (rejected) fails; (unsigned) -1 orders after every index
+    if (t <= tb && (t < tb || (unsigned)sid < (unsigned)best)) {
+        tb = t;
+        best = sid;
     }
 }
 
@@ -330,7 +323,7 @@ struct BvhTrav {
     int ni;    // next node in depth-first order (>= n_nodes: walk finished)
     int pend;  // parked leaf (first | count << 24) or -1
     float tb;  // nearest root so far
-    int best;  // encoded winner (scene_id_of)
+    int best;  // winner's scene index or -1
 };
 
 // Start a scan: the huge spheres (tested linearly, first), then the BVH.
@@ -341,8 +334,7 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.tb = kInf;
     tr.best = -1;
     for (int k = 0; k < A.n_big; ++k)
-        update_lex(A, root_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), -2 - A.big_id[k], tr.tb,
-                   tr.best);
+        update_lex(root_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
     tr.ni = 0;
@@ -402,8 +394,11 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, f3 o, f3 d, BvhTrav &tr
     const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
     if constexpr (kCount)
         cnt.spheres += nl;
-    for (int j = 0; j < nl; ++j)
-        update_lex(A, root_lex<false>(A.bvh_sph[first + j], float4{}, o, d, a, tr.tb), first + j, tr.tb, tr.best);
+    for (int j = 0; j < nl; ++j) {
+        const float t = root_lex<false>(A.bvh_sph[first + j], float4{}, o, d, a, tr.tb);
+        if (t <= tr.tb)  // the scene index is read only for a candidate that wins or ties
+            update_lex(t, A.bvh_id[first + j], tr.tb, tr.best);
+    }
     tr.pend = -1;
 }
 
@@ -421,7 +416,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
             bvh_leaf<kCount>(A, o, d, tr, cnt);
     }
     tbest = tr.tb;
-    return scene_id_of(A, tr.best);
+    return tr.best;
 }
 
 // Per-lane state machine: one call = one bounce segment of radiance()
@@ -586,11 +581,15 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
     LinRec *lds_lin = reinterpret_cast<LinRec *>(dyn_lds);
     const LinRec *recs = A.lin;
-    __shared__ float2 lds_trig[kTrigEntries];
-    static_assert(kTrigEntries <= kBlock, "one table entry per thread");
-    if (threadIdx.x < kTrigEntries)
-        lds_trig[threadIdx.x] = A.trig[threadIdx.x];
+    // linear kernel: the sin/cos table in LDS; the BVH kernel (latency bound
+    // on its node loads) reads it from global memory (L1): measured the same
+    const float2 *trig = A.trig;
     if constexpr (kLdsGeo) {
+        __shared__ float2 lds_trig[kTrigEntries];
+        static_assert(kTrigEntries <= kBlock, "one table entry per thread");
+        if (threadIdx.x < kTrigEntries)
+            lds_trig[threadIdx.x] = A.trig[threadIdx.x];
+        trig = lds_trig;
         for (int i = threadIdx.x; i <= A.n; i += kBlock)  // n records + the sentinel
             lds_lin[i] = A.lin[i];
         recs = lds_lin;
@@ -769,7 +768,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
             if (item >= 0) {
                 if constexpr (kCount)
                     segs += 1;
-                if (segment<kBvh, kCount>(A, recs, lds_trig, o, d, T, E, depth, st, scnt))
+                if (segment<kBvh, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
                     path_done();
             }
             refill();
@@ -815,6 +814,9 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                     }
 #endif
                     if (8 * nh >= PTG_LEAF_FRAC * nt) {  // leaf phase
+                        // (spreading the parked leaves' spheres over the whole wave with
+                        // ds_bpermute + LDS atomicMin measured 1.7 % slower: the leaf
+                        // tests are cheap next to the node steps' memory latency)
                         if (trv && tr.pend >= 0)
                             bvh_leaf<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt);
                     } else if (trv && tr.pend < 0) {  // node step
@@ -826,8 +828,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
             }
             if (item >= 0 && phase == 2) {
                 phase = 0;
-                const int id = scene_id_of(A, tr.best);
-                if (shade(id >= 0 ? A.shade + id : nullptr, tr.tb, lds_trig, o, d, T, E, depth, st))
+                if (shade(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, A.trig, o, d, T, E, depth, st))
                     path_done();
             }
             refill();
