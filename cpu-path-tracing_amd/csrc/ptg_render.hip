@@ -800,7 +800,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                     if (8 * (na - nt) >= PTG_READY_FRAC * na)
                         break;
                     const int nh = (int)__popcll(__ballot(trv && tr.pend >= 0));
-#if PTG_WAVE_STATS  // debug: wave-level node steps / leaf sphere iterations (first active lane only)
+#if PTG_WAVE_STATS == 1  // debug: wave-level node steps / leaf sphere iterations (first active lane only)
                     if constexpr (kCount) {
                         const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
                         if (8 * nh >= PTG_LEAF_FRAC * nt) {
@@ -826,6 +826,13 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                         phase = 2;
                 }
             }
+#if PTG_WAVE_STATS == 2  // debug: wave-level main-loop iterations / iterations that shade (first active lane)
+            if constexpr (kCount) {
+                const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
+                scnt.boxes += first_lane ? 1 : 0;
+                scnt.spheres += (first_lane && __ballot(item >= 0 && phase == 2) != 0ull) ? 1 : 0;
+            }
+#endif
             if (item >= 0 && phase == 2) {
                 phase = 0;
                 if (shade(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, A.trig, o, d, T, E, depth, st))
