@@ -1211,10 +1211,15 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
+    // BVH scenes aim at 4x as many: their cost varies strongly over the image
+    // (10,000-sphere scene: sky rows vs the sphere field), and shorter units
+    // shorten the tail of expensive rows (measured: 64-sample units 551 ms vs
+    // 573 ms for whole-pixel units; on box_scene whole-pixel units are best).
     const int groups = A.slab_rows * A.waves_per_row;
     int chunk = p->chunk_samples;
     if (chunk <= 0) {
-        long long want = (98304 + groups - 1) / groups;
+        const long long target = ctx->n > kLinearMax ? 4 * 98304 : 98304;
+        long long want = (target + groups - 1) / groups;
         long long nch = want < 1 ? 1 : (want > nsamp ? nsamp : want);
         chunk = nch > 0 ? (int)((nsamp + nch - 1) / nch) : 1;
     }
