@@ -231,9 +231,96 @@ def synthetic_scene(n: int, w: int, h: int, gen_seed: int = 42) -> scene:
 
 SCENES = {"simple": simple_scene, "box": box_scene, "box_mirror": box_mirror_scene}
 
+# ---- scene files (the reference hard-codes its scene,
+# main.cpp:25,199-208).  Same format as host/pt/scene_file.hpp:
+#   camera <pos x y z> <look-at x y z> <up x y z> <vfov radians> <aperture> <focus | auto>
+#   sphere <radius> <pos x y z> <emission r g b> <colour r g b> <diffuse|specular|dielectric>
+# '#' starts a comment; aspect ratio = w/h; "auto" focus = |pos - look-at|.
+# Numbers are written with 17 significant digits: save -> load is exact.
+
+_MATERIALS = {"diffuse": reflection_type.diffuse, "specular": reflection_type.specular,
+              "dielectric": reflection_type.dielectric}
+
+
+class SceneFileError(ValueError):
+    pass
+
+
+def parse_scene_text(text: str, w: int, h: int) -> scene:
+    scn = scene()
+    have_camera = False
+    for lineno, raw in enumerate(text.splitlines(), 1):
+        tok = raw.split("#", 1)[0].split()
+        if not tok:
+            continue
+
+        def bad(why):
+            return SceneFileError(f"line {lineno}: {why}")
+
+        nnum = {"camera": 11, "sphere": 10}.get(tok[0])
+        if nnum is None:
+            raise bad(f"unknown item '{tok[0]}' (camera | sphere)")
+        if len(tok) != nnum + 2:
+            raise bad(f"{tok[0]} needs {nnum + 1} fields")
+        try:
+            v = [float(t) for t in tok[1:nnum + 1]]
+        except ValueError as e:
+            raise bad(f"not a number: {e}") from None
+        if tok[0] == "camera":
+            if have_camera:
+                raise bad("second camera")
+            have_camera = True
+            c = scn.camera_parameters
+            c.position, c.direction, c.up = tuple(v[0:3]), tuple(v[3:6]), tuple(v[6:9])
+            c.vertical_fov_radians, c.aperture = v[9], v[10]
+            c.aspect_ratio = (w * 1.0) / (h * 1.0)
+            if tok[12] == "auto":
+                c.focus_distance = length(_sub(c.position, c.direction))
+            else:
+                try:
+                    c.focus_distance = float(tok[12])
+                except ValueError:
+                    raise bad("focus distance must be a number or 'auto'") from None
+        else:
+            if tok[11] not in _MATERIALS:
+                raise bad("material must be diffuse, specular or dielectric")
+            if not v[0] > 0.0:
+                raise bad("radius must be positive")
+            scn.spheres.append(sphere(v[0], tuple(v[1:4]), tuple(v[4:7]), tuple(v[7:10]), _MATERIALS[tok[11]]))
+    if not have_camera:
+        raise SceneFileError("no camera line")
+    return scn
+
+
+def load_scene_file(path: str, w: int, h: int) -> scene:
+    with open(path) as f:
+        return parse_scene_text(f.read(), w, h)
+
+
+def scene_text(scn: scene) -> str:
+    f = lambda x: "%.17g" % x  # noqa: E731
+    v3 = lambda a: " ".join(f(x) for x in a)  # noqa: E731
+    names = {0: "diffuse", 1: "specular", 2: "dielectric"}
+    c = scn.camera_parameters
+    out = ["# pt-scene: camera pos look-at up vfov aperture focus; sphere radius pos emission colour material",
+           f"camera {v3(c.position)}  {v3(c.direction)}  {v3(c.up)}  {f(c.vertical_fov_radians)} "
+           f"{f(c.aperture)} {f(c.focus_distance)}"]
+    for s in scn.spheres:
+        out.append(f"sphere {f(s.radius)}  {v3(s.position)}  {v3(s.emission)}  {v3(s.color)}  "
+                   f"{names[int(s.reflection)]}")
+    return "\n".join(out) + "\n"
+
+
+def save_scene_file(scn: scene, path: str) -> None:
+    with open(path, "w") as f:
+        f.write(scene_text(scn))
+
 
 def make_scene(name: str, w: int, h: int) -> scene:
+    """A built-in scene (simple, box, box_mirror, synthetic[:N]) or a scene file."""
     if name.startswith("synthetic"):
         n = int(name.split(":")[1]) if ":" in name else 10000
         return synthetic_scene(n, w, h)
-    return SCENES[name](w, h)
+    if name in SCENES:
+        return SCENES[name](w, h)
+    return load_scene_file(name, w, h)

@@ -284,3 +284,44 @@ def test_progressive_accumulation_matches_one_shot():
             _check_equal(img, ref)
         one, _ = _gpu_image(scn, cam, W, H, samps)
         assert np.array_equal(img, one)
+
+
+def test_scene_file_renders_like_the_builtin_scene(tmp_path):
+    """f4: a scene written to a file and read back renders the same bits."""
+    _require_gpu()
+    W, H, samps = 48, 32, 8
+    scn = ptgpu.box_mirror_scene(W, H)
+    path = tmp_path / "mirror.scene"
+    ptgpu.save_scene_file(scn, str(path))
+    back = ptgpu.make_scene(str(path), W, H)
+    a, _ = _gpu_image(scn, ptgpu.camera.with_config(scn.camera_parameters), W, H, samps)
+    b, _ = _gpu_image(back, ptgpu.camera.with_config(back.camera_parameters), W, H, samps)
+    assert np.array_equal(a, b)
+
+
+def test_cli_renders_and_splits_over_devices(tmp_path):
+    """The C++ CLI (host/main.cpp): one thread per listed device renders the
+    interleaved rows k mod N; two shards on the same GPU give the same P6
+    bytes as one, and those are the reference's color_to_int of the drop-in
+    image (utils.cpp:11-16)."""
+    _require_gpu()
+    import os
+    import subprocess
+    cli = os.path.join(os.path.dirname(ptgpu.LIB_PATH), "pt_render_gpu")
+    W, H, spp = 40, 30, 16
+    outs = {}
+    for devs in ("0", "0,0"):
+        out = tmp_path / f"img_{devs.replace(',', '_')}.ppm"
+        r = subprocess.run([cli, "--scene", "box", "--width", str(W), "--height", str(H), "--spp", str(spp),
+                            "--devices", devs, "--format", "p6", "--out", str(out)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs[devs] = out.read_bytes()
+    assert outs["0"] == outs["0,0"]
+    header = f"P6\n{W} {H}\n255\n".encode()
+    assert outs["0"].startswith(header)
+    scn = ptgpu.box_scene(W, H)
+    img = np.zeros((H * W, 3))
+    ptgpu.render(scn, ptgpu.camera.with_config(scn.camera_parameters), img, W, H, spp // 4)
+    ref = po.tonemap(img).astype(np.uint8).tobytes()
+    assert outs["0"][len(header):] == ref
