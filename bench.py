@@ -81,16 +81,20 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s):
                        f"reference arithmetic) in an OpenMP schedule(dynamic,1) row loop")}
 
 
-def load_traffic(workload):
+def load_pmc(workload):
+    """PMC figures of the committed rocprofv3 profile of this workload
+    (profiles/pmc_traffic.json, written by profiles/summarize.py): HBM bytes
+    per launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section)
+    and the VALU issue utilisation."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
         if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+            return d
     except (OSError, ValueError):
         pass
-    return None
+    return {}
 
 
 def main():
@@ -202,7 +206,8 @@ def main():
         cpu = None
         if world == 1 and args.cpu_baseline == "auto":
             cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads, args.cpu_seconds)
-        traffic = load_traffic(workload)
+        pmc = load_pmc(workload)
+        traffic = pmc.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -230,7 +235,13 @@ def main():
                          "segments_per_sample": round(s_bar, 4),
                          "sphere_tests_per_segment": round(tests_per_sample / s_bar, 2) if s_bar else None,
                          "box_tests_per_segment": round(boxes_per_sample / s_bar, 2) if s_bar else None,
-                         "scan": "bvh" if n_sph > 64 else "linear"},
+                         "scan": "bvh" if n_sph > 64 else "linear",
+                         # measured issue-side view (rocprofv3 profile of this workload,
+                         # profiles/<tag>_summary.json): wave64 VALU instructions x 2 cycles
+                         # over the 1,024 SIMDs' cycles -- the hardware bound the FLOP model
+                         # above does not see
+                         "valu_issue_pct_profiled": pmc.get("valu_issue_pct"),
+                         "profile": pmc.get("tag")},
             "cpu_baseline": cpu,
         }
         if cpu:

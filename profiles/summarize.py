@@ -78,9 +78,16 @@ def main(src, tag, kernel_sub="render_kernel"):
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     shutil.copy(stats, os.path.join(os.path.dirname(dst), f"{tag}_kernel_stats.csv"))
+    rec = {"workload": out.get("bench", {}).get("config", {}).get("workload"), "tag": tag,
+           "hbm_bytes_per_launch": round(fetch_b + write_b)}
+    if "derived" in out:
+        rec["valu_issue_pct"] = round(out["derived"]["valu_issue_pct"], 1)
+        rec["valu_lane_utilisation_pct"] = round(out["derived"]["VALUUtilization_pct"], 1)
+        rec["clock_GHz"] = round(out["derived"]["clock_GHz"], 3)
+    if "valu_insts_per_segment_wave_level" in out:
+        rec["valu_insts_per_64_lane_segments"] = round(out["valu_insts_per_segment_wave_level"], 1)
     with open(os.path.join(os.path.dirname(dst), "pmc_traffic.json"), "w") as f:
-        json.dump({"workload": out.get("bench", {}).get("config", {}).get("workload"), "tag": tag,
-                   "hbm_bytes_per_launch": round(fetch_b + write_b)}, f)
+        json.dump(rec, f)
     print(json.dumps(out, indent=1)[:3000])
 
 
