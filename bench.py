@@ -42,9 +42,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s):
+def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s, gpu_image=None, seed=None, quality_rows=4):
     """Time the repo's OpenMP CPU path (oracle Mode A: reference arithmetic,
-    double + mt19937 row seeding) on a bounded subset of the frame's rows."""
+    double + mt19937 row seeding) on a bounded subset of the frame's rows.
+
+    With `gpu_image` (the benchmarked frame, [H, W, 3] float32) the same leg
+    also checks quality on `quality_rows` evenly spaced rows:
+    per-pixel RMSE and max |diff| of the GPU image against the identically
+    seeded fp32 CPU restatement (Mode B, the checker: 0 when bit-exact), and
+    the RMSE of that against the same path in double arithmetic with the same
+    counter RNG (Mode A/xs) -- the effect of computing in fp32."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import pyoracle as po
@@ -74,11 +81,29 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s):
             break
     dt = time.perf_counter() - t0
     nsamp = rows * W * samps * nsub * nsub
-    return {"value": round(nsamp / dt / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "port",
-            "seconds": round(dt, 2),
-            "sample": (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp, {rows} of {H} rows "
-                       f"(y = k mod 64 for k in {offsets}); oracle Mode A (double, mt19937 per row, "
-                       f"reference arithmetic) in an OpenMP schedule(dynamic,1) row loop")}
+    out = {"value": round(nsamp / dt / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "port",
+           "seconds": round(dt, 2),
+           "sample": (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp, {rows} of {H} rows "
+                      f"(y = k mod 64 for k in {offsets}); oracle Mode A (double, mt19937 per row, "
+                      f"reference arithmetic) in an OpenMP schedule(dynamic,1) row loop")}
+    if gpu_image is not None and quality_rows > 0:
+        step_y = max(1, H // quality_rows)
+        ys = np.arange(step_y // 2, H, step_y)[:quality_rows]  # image-space y (main.cpp:181: y = 0 at the bottom)
+        t1 = time.perf_counter()
+        gpu = np.concatenate([gpu_image[H - 1 - y] for y in ys]).astype(np.float64)
+        b = np.concatenate([po.render_xs_f32(sp, ca, W, H, samps, nsub, seed, rows=(int(y), int(y) + 1, 1),
+                                             nthreads=threads)[0][H - 1 - y] for y in ys]).astype(np.float64)
+        a = np.concatenate([po.render_xs_f64(sp, ca, W, H, samps, nsub, seed, rows=(int(y), int(y) + 1, 1),
+                                             nthreads=threads)[0][H - 1 - y] for y in ys])
+        out["quality"] = {
+            "rows": [int(y) for y in ys],
+            "rmse_vs_cpu_fp32": float(np.sqrt(((gpu - b) ** 2).mean())),
+            "max_abs_vs_cpu_fp32": float(np.abs(gpu - b).max()),
+            "rmse_fp32_vs_fp64_same_rng": float(np.sqrt(((b - a) ** 2).mean())),
+            "image_mean": float(gpu.mean()),
+            "seconds": round(time.perf_counter() - t1, 2),
+            "checker": "oracle Mode B (fp32 restatement) / Mode A-xs (double, same counter RNG)"}
+    return out
 
 
 def load_pmc(workload):
@@ -111,6 +136,8 @@ def main():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--quality-rows", type=int, default=4,
+                    help="rows checked against the CPU oracle in the cpu_baseline leg (0 = none)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,7 +232,9 @@ def main():
         value = frame_samples * args.steps / elapsed / 1e6
         cpu = None
         if world == 1 and args.cpu_baseline == "auto":
-            cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads, args.cpu_seconds)
+            frame = slab.cpu().numpy().reshape(rows, W, 3)[:H]  # band_rows = 1, one shard: slab row = image row
+            cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads, args.cpu_seconds, frame,
+                               ptgpu.DEFAULT_SEED, args.quality_rows)
         pmc = load_pmc(workload)
         traffic = pmc.get("hbm_bytes_per_launch")
         out = {
@@ -216,6 +245,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "segments_per_s": round(value * 1e6 * s_bar, 1),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
