@@ -49,6 +49,15 @@ int fail(int code, const std::string &msg)
         if (e_ != hipSuccess)                                                                      \
             return fail(PTG_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));           \
     } while (0)
+// inside ptg_context_create, once `ctx` exists: release it on failure
+#define PTG_HIP_OR_DESTROY(call)                                                                   \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            ptg_context_destroy(ctx);                                                              \
+            return fail(PTG_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));           \
+        }                                                                                          \
+    } while (0)
 
 constexpr int kBlock = 256;        // 4 waves per workgroup
 #ifndef PTG_MAX_LDS_SPHERES
@@ -1313,9 +1322,9 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the scene failed");
     }
     if (linear)
-        PTG_HIP(hipMemcpy(ctx->d_lin, lin.data(), bytes, hipMemcpyHostToDevice));
+        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_lin, lin.data(), bytes, hipMemcpyHostToDevice));
     else if (n_spheres)
-        PTG_HIP(hipMemcpy(ctx->d_shade, shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
+        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade, shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
     {
         float tab[2 * kTrigEntries];
         trig_table(tab);
@@ -1323,7 +1332,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             ptg_context_destroy(ctx);
             return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the sin/cos table failed");
         }
-        PTG_HIP(hipMemcpy(ctx->d_trig, tab, sizeof(tab), hipMemcpyHostToDevice));
+        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_trig, tab, sizeof(tab), hipMemcpyHostToDevice));
     }
     KArgs &A = ctx->base;
     std::memset(&A, 0, sizeof(A));
@@ -1367,7 +1376,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             ptg_context_destroy(ctx);
             return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the BVH failed");
         }
-        PTG_HIP(hipMemcpy(ctx->d_bvh, blob.data(), total, hipMemcpyHostToDevice));
+        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_bvh, blob.data(), total, hipMemcpyHostToDevice));
         unsigned char *base = static_cast<unsigned char *>(ctx->d_bvh);
         A.bvh_nodes = reinterpret_cast<const float4 *>(base);
         A.bvh_qnodes = reinterpret_cast<const uint4 *>(base + off_q);

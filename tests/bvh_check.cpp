@@ -1,0 +1,123 @@
+// Host-side check of the BVH builder (cpu-path-tracing_amd/csrc/bvh_build.hpp),
+// built and run by tests/test_bvh_builder.py with AddressSanitizer/UBSan.
+// For random scenes it verifies the invariants the GPU traversal relies on
+// (see ptg_render.hip: bvh_node_step):
+//   * every non-huge sphere sits in exactly one leaf, huge spheres in `big`;
+//   * depth-first layout: a node's subtree is the index range [i, skip);
+//     leaves have skip = i + 1; inner nodes' children are i + 1 and the
+//     node after the first child's subtree;
+//   * every box contains its subtree's spheres (centre +- radius) and its
+//     children's boxes (culling can never drop a candidate);
+//   * the 16-bit quantised boxes, decoded on the grid, contain the float boxes.
+// Prints "ok <nodes>" per scene; exits non-zero on the first violation.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../cpu-path-tracing_amd/csrc/bvh_build.hpp"
+
+using namespace ptg;
+
+static int fails = 0;
+#define CHECK(c, ...)                                                                              \
+    do {                                                                                           \
+        if (!(c)) {                                                                                \
+            std::fprintf(stderr, __VA_ARGS__);                                                     \
+            std::fprintf(stderr, "\n");                                                            \
+            ++fails;                                                                               \
+            return;                                                                                \
+        }                                                                                          \
+    } while (0)
+
+static void check_scene(const std::vector<ptg_sphere> &s)
+{
+    const int n = (int)s.size();
+    BvhBuild b = build_bvh(s.data(), n, 1000.0);
+    std::vector<int> seen(n, 0);
+    for (int i : b.big)
+        seen[i] += 1;
+    for (int i : b.order)
+        seen[i] += 10;
+    for (int i = 0; i < n; ++i) {
+        const bool huge = s[i].radius >= 1000.0;
+        CHECK(seen[i] == (huge ? 1 : 10), "sphere %d placed %d (huge %d)", i, seen[i], (int)huge);
+    }
+    const int nn = (int)b.nodes.size();
+    // subtree ranges and containment
+    std::vector<int> leaf_cover(b.order.size(), 0);
+    for (int i = 0; i < nn; ++i) {
+        const BvhNodeHost &nd = b.nodes[i];
+        CHECK(nd.skip > i && nd.skip <= nn, "node %d skip %d", i, nd.skip);
+        if (nd.leaf >= 0) {
+            CHECK(nd.skip == i + 1, "leaf %d skip %d", i, nd.skip);
+            const int first = nd.leaf & 0xFFFFFF, cnt = nd.leaf >> 24;
+            CHECK(cnt >= 1 && cnt <= kLeafSize && first + cnt <= (int)b.order.size(), "leaf %d range", i);
+            for (int k = first; k < first + cnt; ++k) {
+                leaf_cover[k] += 1;
+                const ptg_sphere &sp = s[b.order[k]];
+                for (int c = 0; c < 3; ++c)
+                    CHECK(nd.bmin[c] <= sp.position[c] - sp.radius && nd.bmax[c] >= sp.position[c] + sp.radius,
+                          "leaf %d does not contain sphere %d (axis %d)", i, b.order[k], c);
+            }
+        } else {
+            CHECK(i + 1 < nd.skip, "inner node %d has no children", i);
+            const int l = i + 1, r = b.nodes[l].skip;
+            CHECK(r < nd.skip && b.nodes[r].skip == nd.skip, "inner node %d children %d %d", i, l, r);
+            for (int ch : {l, r})
+                for (int c = 0; c < 3; ++c)
+                    CHECK(nd.bmin[c] <= b.nodes[ch].bmin[c] && nd.bmax[c] >= b.nodes[ch].bmax[c],
+                          "node %d does not contain child %d", i, ch);
+        }
+    }
+    for (size_t k = 0; k < leaf_cover.size(); ++k)
+        CHECK(leaf_cover[k] == 1, "leaf slot %zu covered %d times", k, leaf_cover[k]);
+    // quantised boxes contain the float boxes
+    std::vector<BvhNodeQ> q;
+    const BvhGrid g = quantise_bvh(b.nodes, q);
+    CHECK(q.size() == b.nodes.size(), "quantised node count");
+    for (int i = 0; i < nn; ++i) {
+        const BvhNodeQ &z = q[i];
+        const unsigned qv[6] = {z.xy_min & 0xFFFFu, z.xy_min >> 16, z.z_min_x_max & 0xFFFFu,
+                                z.z_min_x_max >> 16, z.y_max_z_max & 0xFFFFu, z.y_max_z_max >> 16};
+        const double lo[3] = {g.lo[0] + qv[0] * (double)g.scale[0], g.lo[1] + qv[1] * (double)g.scale[1],
+                              g.lo[2] + qv[2] * (double)g.scale[2]};
+        const double hi[3] = {g.lo[0] + qv[3] * (double)g.scale[0], g.lo[1] + qv[4] * (double)g.scale[1],
+                              g.lo[2] + qv[5] * (double)g.scale[2]};
+        for (int c = 0; c < 3; ++c)
+            CHECK(lo[c] <= b.nodes[i].bmin[c] && hi[c] >= b.nodes[i].bmax[c], "quantised node %d axis %d", i, c);
+        const BvhNodeHost &nd = b.nodes[i];
+        if (nd.leaf >= 0)
+            CHECK(z.word < 0 && (z.word & 0x7FFFFFFF) == nd.leaf, "quantised leaf word %d", i);
+        else
+            CHECK(z.word == nd.skip, "quantised skip %d", i);
+    }
+    std::printf("ok %d spheres %d nodes %zu huge\n", n, nn, b.big.size());
+}
+
+int main()
+{
+    std::mt19937 rng(1234);
+    std::uniform_real_distribution<double> u(0.0, 1.0);
+    for (int n : {2, 65, 300, 3000, 20000}) {
+        std::vector<ptg_sphere> s(n);
+        for (int i = 0; i < n; ++i) {
+            ptg_sphere &sp = s[i];
+            std::memset(&sp, 0, sizeof(sp));
+            const bool huge = i % 97 == 0;  // a few huge spheres anywhere in the list
+            sp.radius = huge ? 1e6 : 0.01 + 0.3 * u(rng);
+            for (int c = 0; c < 3; ++c)
+                sp.position[c] = huge ? (c == 1 ? -1e6 : 0.0) : -20.0 + 40.0 * u(rng);
+            if (i % 7 == 0 && !huge)  // clusters of identical centres (median ties)
+                for (int c = 0; c < 3; ++c)
+                    sp.position[c] = 1.0;
+            sp.material = i % 3;
+        }
+        check_scene(s);
+        if (fails)
+            return 1;
+    }
+    return 0;
+}

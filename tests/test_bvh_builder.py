@@ -1,0 +1,24 @@
+"""Host-side BVH builder invariants (cpu-path-tracing_amd/csrc/bvh_build.hpp),
+checked by tests/bvh_check.cpp built with AddressSanitizer + UBSan: sphere
+placement, depth-first skip layout, box containment, and the 16-bit quantised
+boxes containing the float boxes -- what the GPU traversal relies on to never
+drop a candidate (the GPU parity tests check the images end to end)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_bvh_builder_invariants(tmp_path):
+    exe = tmp_path / "bvh_check"
+    src = os.path.join(ROOT, "tests", "bvh_check.cpp")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"), src, "-o", str(exe)])
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 5 and all(line.startswith("ok ") for line in lines), r.stdout
