@@ -82,6 +82,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_FRAC
 #define PTG_LEAF_FRAC 6  // BVH: leaf phase once 6/8 of the walking lanes hold a leaf (measured: 6 beats 4 by 2 %)
 #endif
+#ifndef PTG_BVH_UNIT_MULT
+#define PTG_BVH_UNIT_MULT 4  // BVH scenes: aim at this many times more work units
+#endif
+#ifndef PTG_TAIL_CHUNKS
+#define PTG_TAIL_CHUNKS 8  // split-tail units per pixel group of the last rows (1: off)
+#endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 4  // BVH: stop walking and shade once 4/8 of the active lanes have finished their scan
 #endif
@@ -126,6 +132,11 @@ struct KArgs {
     float invW, invH, inv_samps, sub_len, inv_sub2;
     unsigned long long seed;
     int chunk, n_groups, single_chunk;
+    // split tail (fill_launch): groups [tail_group, n_groups) -- the last rows
+    // -- run as tail_chunks units of tail_chunk samples each (accumulated,
+    // then resolve_kernel from slab row resolve_row0); tail_group = n_groups
+    // when the whole grid is one kind of unit
+    int tail_group, n_head_chunks, tail_chunk, resolve_row0;
     int sample_begin, sample_end;  // samples [begin, end) of every sub-pixel in this launch
     int keep_acc;                  // resolve without re-zeroing (progressive previews)
     int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
@@ -611,8 +622,25 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     const long long unit = (long long)blockIdx.x * kWavesPerBlock + wv;
     if (unit >= A.n_units)
         return;  // whole wave
-    const int group = (int)(unit % A.n_groups);  // chunk-major: neighbours are different pixel groups
-    const int chunk = (int)(unit / A.n_groups);
+    // head units: groups [0, tail_group) x n_head_chunks chunks of A.chunk
+    // samples, chunk-major (neighbours are different pixel groups); then the
+    // split tail (fill_launch): the last groups in chunks of A.tail_chunk
+    const long long head_units = (long long)A.tail_group * A.n_head_chunks;
+    int group, s0, len;
+    bool in_wave;  // the unit holds every sample of its pixels: resolve in the wave
+    if (unit < head_units) {
+        group = (int)(unit % A.tail_group);
+        s0 = A.sample_begin + (int)(unit / A.tail_group) * A.chunk;
+        len = A.chunk;
+        in_wave = A.single_chunk;
+    } else {
+        const long long t = unit - head_units;
+        const int ntail = A.n_groups - A.tail_group;
+        group = A.tail_group + (int)(t % ntail);
+        s0 = A.sample_begin + (int)(t / ntail) * A.tail_chunk;
+        len = A.tail_chunk;
+        in_wave = false;
+    }
     const int slab_row = group / A.waves_per_row;
     const int xblk = group - slab_row * A.waves_per_row;
     const int r = out_row_of(A, slab_row);
@@ -621,9 +649,8 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     int npix = A.W - x0;
     npix = npix < A.pixels_per_wave ? npix : A.pixels_per_wave;
     const int nv = r < A.H ? npix * A.lanes_per_pixel : 0;  // valid slots are a prefix
-    const int s0 = A.sample_begin + chunk * A.chunk;
     int cnt = A.sample_end - s0;
-    cnt = cnt < A.chunk ? cnt : A.chunk;
+    cnt = cnt < len ? cnt : len;
     const int total = nv * cnt;
 
     lds_acc[wv][lane] = 0ull;
@@ -868,7 +895,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (A.single_chunk) {
+    if (in_wave) {
         // the unit holds every sample of its pixels: resolve in the wave
         // (main.cpp:195-196, same arithmetic as resolve_kernel) and write
         // 12 B per pixel -- the only HBM traffic of the frame
@@ -904,7 +931,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
 // 1/nsub^2 in (sy, sx) order; re-zeroes the accumulator for the next frame.
 __global__ __launch_bounds__(256) void resolve_kernel(KArgs A)
 {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long i = (long long)A.resolve_row0 * A.W + (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= (long long)A.slab_rows * A.W)
         return;
     const int slab_row = (int)(i / A.W);
@@ -994,6 +1021,7 @@ __global__ void tonemap_kernel(const float *__restrict__ in, uint8_t *__restrict
 struct ptg_context {
     int device;
     int n;
+    int wave_slots;     // CUs x 32 resident waves (split-tail sizing)
     LinRec *d_lin;      // linear scenes
     ShadeRec *d_shade;  // BVH scenes
     void *d_bvh;  // one allocation: nodes | leaf geometry | leaf ids | big geometry | big ids
@@ -1227,7 +1255,7 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     const int groups = A.slab_rows * A.waves_per_row;
     int chunk = p->chunk_samples;
     if (chunk <= 0) {
-        const long long target = ctx->n > kLinearMax ? 4 * 98304 : 98304;
+        const long long target = ctx->n > kLinearMax ? PTG_BVH_UNIT_MULT * 98304 : 98304;
         long long want = (target + groups - 1) / groups;
         long long nch = want < 1 ? 1 : (want > nsamp ? nsamp : want);
         chunk = nch > 0 ? (int)((nsamp + nch - 1) / nch) : 1;
@@ -1240,6 +1268,25 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     // in-wave resolve only when one unit holds ALL samples of its pixels
     A.single_chunk = !accumulate_only && n_chunks <= 1 && s_begin == 0 && s_end == p->samples;
     A.n_units = (long long)A.n_groups * n_chunks;
+    A.tail_group = groups;
+    A.n_head_chunks = n_chunks;
+    A.tail_chunk = chunk;
+    A.resolve_row0 = 0;
+    // Split tail: with whole-pixel units, the grid ends when its slowest last
+    // units end (a unit is ~1/16 of the frame per wave slot here).  The last
+    // rows -- about one round of the device's wave slots -- run instead as
+    // PTG_TAIL_CHUNKS shorter units each, accumulated and resolved by
+    // resolve_kernel; everything before keeps the in-wave resolve.
+    if (A.single_chunk && p->chunk_samples <= 0 && PTG_TAIL_CHUNKS > 1 && nsamp >= PTG_TAIL_CHUNKS &&
+        groups >= 4 * ctx->wave_slots) {
+        const int tail_rows = (ctx->wave_slots + A.waves_per_row - 1) / A.waves_per_row;
+        A.tail_group = (A.slab_rows - tail_rows) * A.waves_per_row;
+        A.n_head_chunks = 1;
+        A.tail_chunk = (nsamp + PTG_TAIL_CHUNKS - 1) / PTG_TAIL_CHUNKS;
+        const int tail_chunks = (nsamp + A.tail_chunk - 1) / A.tail_chunk;
+        A.resolve_row0 = A.slab_rows - tail_rows;
+        A.n_units = (long long)A.tail_group + (long long)(groups - A.tail_group) * tail_chunks;
+    }
     grid = (int)((A.n_units + kWavesPerBlock - 1) / kWavesPerBlock);
 }
 
@@ -1314,6 +1361,10 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     }
     ptg_context *ctx = new ptg_context();
     ctx->device = dev;
+    {
+        hipDeviceProp_t prop;
+        ctx->wave_slots = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount * 32 : 8192;
+    }
     ctx->n = (int)n_spheres;
     // linear scenes: d_lin; BVH scenes: d_shade (scene index order) + d_bvh
     const size_t bytes = linear ? lin.size() * sizeof(LinRec) : std::max<size_t>(n_spheres, 1) * sizeof(ShadeRec);
@@ -1485,7 +1536,9 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
 
 int launch_resolve(const KArgs &A, hipStream_t s)
 {
-    long long pixels = (long long)A.slab_rows * A.W;
+    long long pixels = (long long)(A.slab_rows - A.resolve_row0) * A.W;
+    if (pixels <= 0)
+        return PTG_OK;
     resolve_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>(A);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
@@ -1507,7 +1560,8 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     KArgs A;
     int grid = 0;
     fill_launch(ctx, params, A, grid);
-    const bool resolve = !A.single_chunk || grid == 0;  // several units per pixel, or no samples at all
+    // several units per pixel, a split tail, or no samples at all
+    const bool resolve = !A.single_chunk || A.tail_group < A.n_groups || grid == 0;
     if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
         return rc;
     A.out = d_slab;
@@ -1557,6 +1611,7 @@ int ptg_resolve_device(ptg_context *ctx, const ptg_params *params, int32_t sampl
         return rc;
     A.samps = samples_done;  // mean over the samples accumulated so far
     A.keep_acc = 1;
+    A.resolve_row0 = 0;  // every row (the one-shot split tail does not apply here)
     A.acc = ctx->d_acc;
     A.out = d_slab;
     return launch_resolve(A, reinterpret_cast<hipStream_t>(stream));
