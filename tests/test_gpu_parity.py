@@ -325,3 +325,21 @@ def test_cli_renders_and_splits_over_devices(tmp_path):
     ptgpu.render(scn, ptgpu.camera.with_config(scn.camera_parameters), img, W, H, spp // 4)
     ref = po.tonemap(img).astype(np.uint8).tobytes()
     assert outs["0"][len(header):] == ref
+
+
+def test_split_tail_frame_is_exact():
+    """A large frame with whole-pixel units runs its last rows as the split
+    tail (8 accumulated units per pixel group + resolve_kernel for those rows,
+    fill_launch): the image equals the same frame with every pixel group split
+    into explicit chunks, and the oracle on rows of both regions."""
+    _require_gpu()
+    W, H, samps = 1920, 1080, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    tail, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    chunked, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1, chunk=3)
+    assert np.array_equal(tail, chunked)
+    sp, ca = _oracle_scene(scn, cam)
+    for y in (0, 1, 2, 537, H - 1):  # y = 0.. are the bottom image rows = the last slab rows (the tail)
+        ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
+        _check_equal(tail[H - 1 - y], ref[H - 1 - y])
