@@ -40,6 +40,7 @@ struct BvhBuild {
     std::vector<BvhNodeHost> nodes;
     std::vector<int32_t> order;  // leaf-ordered sphere indices (into the scene)
     std::vector<int32_t> big;    // huge spheres, tested linearly
+    std::vector<int8_t> axis;    // per node: split axis of an inner node (its first child is the low side), -1 leaf
 };
 
 namespace detail {
@@ -62,6 +63,7 @@ inline int build_rec(const ptg_sphere *s, std::vector<int32_t> &idx, int lo, int
     }
     const int me = (int)b.nodes.size();
     b.nodes.push_back(BvhNodeHost{});
+    b.axis.push_back(-1);
     {
         BvhNodeHost &n = b.nodes[me];
         for (int c = 0; c < 3; ++c) {
@@ -87,13 +89,43 @@ inline int build_rec(const ptg_sphere *s, std::vector<int32_t> &idx, int lo, int
         return s[a].position[axis] < s[c].position[axis] || (s[a].position[axis] == s[c].position[axis] && a < c);
     });
     b.nodes[me].leaf = -1;
+    b.axis[me] = (int8_t)axis;
     build_rec(s, idx, lo, mid, b);
     build_rec(s, idx, mid, hi, b);
     b.nodes[me].skip = (int)b.nodes.size();
     return me;
 }
 
+inline void order_rec(const BvhBuild &b, int i, int octant, std::vector<BvhNodeHost> &out)
+{
+    const int me = (int)out.size();
+    out.push_back(b.nodes[i]);
+    if (b.nodes[i].leaf >= 0) {
+        out[me].skip = me + 1;
+        return;
+    }
+    const int lo = i + 1, hi = b.nodes[lo].skip;
+    const bool flip = (octant >> b.axis[i]) & 1;
+    order_rec(b, flip ? hi : lo, octant, out);
+    order_rec(b, flip ? lo : hi, octant, out);
+    out[me].skip = (int)out.size();
+}
+
 }  // namespace detail
+
+// The same tree in depth-first order for rays of one direction octant (bit k
+// set: d_k < 0): at every inner node the child on the side the ray comes
+// from is walked first, so the nearest hit usually shrinks the culling
+// distance before the far child's boxes are tested.  Same nodes and leaves;
+// skip indices recomputed.  Octant 0 is build_bvh's own order.
+inline std::vector<BvhNodeHost> order_bvh(const BvhBuild &b, int octant)
+{
+    std::vector<BvhNodeHost> out;
+    out.reserve(b.nodes.size());
+    if (!b.nodes.empty())
+        detail::order_rec(b, 0, octant, out);
+    return out;
+}
 
 inline BvhBuild build_bvh(const ptg_sphere *s, int n, double big_radius)
 {

@@ -88,6 +88,15 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_TAIL_CHUNKS
 #define PTG_TAIL_CHUNKS 8  // split-tail units per pixel group of the last rows (1: off)
 #endif
+#ifndef PTG_TAIL_MIN_HALF_ROUNDS
+// linear scenes: split tail from 1.5 rounds of wave slots on (measured with
+// tools/shard_sim.py: 2/4/8-way shards of the bench frame 1.6/1.8/1.4 %
+// faster than with their samples split into ~96k units)
+#define PTG_TAIL_MIN_HALF_ROUNDS 3
+#endif
+#ifndef PTG_BVH_OCTANTS
+#define PTG_BVH_OCTANTS 1  // BVH: one depth-first layout per ray-direction octant (near child first)
+#endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 4  // BVH: stop walking and shade once 4/8 of the active lanes have finished their scan
 #endif
@@ -119,6 +128,10 @@ struct KArgs {
     const GeoRec *big_geo;    // huge spheres, tested linearly
     const int *big_id;
     int n_nodes, n_big;
+    // PTG_BVH_OCTANTS: 8 depth-first layouts of the tree (bvh_build.hpp
+    // order_bvh), layout k at node index k << bvh_shift, skip words absolute;
+    // a walk is done when (ni & bvh_mask) reaches n_nodes
+    int bvh_shift, bvh_mask;
     const float2 *trig;  // {cos, sin}(2 pi k / 128), staged in LDS (sincos2pi_tab)
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
     float pos_x, pos_y, pos_z;
@@ -340,13 +353,16 @@ __device__ __forceinline__ void update_lex(const float t, const int sid, float &
 // wave otherwise waits for its slowest ray (measured 93 wave-level node
 // steps for 33 per ray on the 10,000-sphere scene).
 struct BvhTrav {
-    int ni;    // next node in depth-first order (>= n_nodes: walk finished)
+    int ni;    // next node in depth-first order (bvh_done: walk finished)
     int pend;  // parked leaf (first | count << 24) or -1
     float tb;  // nearest root so far
     int best;  // winner's scene index or -1
 };
 
-// Start a scan: the huge spheres (tested linearly, first), then the BVH.
+__device__ __forceinline__ bool bvh_done(const KArgs &A, int ni) { return (ni & A.bvh_mask) >= A.n_nodes; }
+
+// Start a scan: the huge spheres (tested linearly, first), then the BVH in
+// the layout of the ray's direction octant.
 template <bool kCount>
 __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
@@ -357,7 +373,13 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
         update_lex(root_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
+#if PTG_BVH_OCTANTS
+    const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
+                         ((__float_as_uint(d.z) >> 29) & 4u);
+    tr.ni = (int)(oct << A.bvh_shift);
+#else
     tr.ni = 0;
+#endif
     tr.pend = -1;
 }
 
@@ -430,7 +452,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     BvhTrav tr;
     bvh_start<kCount>(A, o, d, tr, cnt);
     const SlabRay sr = slab_ray(A, o, d);
-    while (tr.ni < A.n_nodes) {
+    while (!bvh_done(A, tr.ni)) {
         bvh_node_step<kCount>(A, sr, tr, cnt);
         if (tr.pend >= 0)
             bvh_leaf<kCount>(A, o, d, tr, cnt);
@@ -822,7 +844,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                 if constexpr (kCount)
                     segs += 1;
                 bvh_start<kCount>(A, o, d, tr, scnt);
-                phase = tr.ni < A.n_nodes ? 1 : 2;
+                phase = bvh_done(A, tr.ni) ? 2 : 1;
             }
             {
                 const SlabRay sr = slab_ray(A, o, d);
@@ -858,7 +880,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
                     } else if (trv && tr.pend < 0) {  // node step
                         bvh_node_step<kCount && !PTG_WAVE_STATS>(A, sr, tr, scnt);
                     }
-                    if (trv && tr.pend < 0 && tr.ni >= A.n_nodes)
+                    if (trv && tr.pend < 0 && bvh_done(A, tr.ni))
                         phase = 2;
                 }
             }
@@ -1253,8 +1275,19 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     // shorten the tail of expensive rows (measured: 64-sample units 551 ms vs
     // 573 ms for whole-pixel units; on box_scene whole-pixel units are best).
     const int groups = A.slab_rows * A.waves_per_row;
+    // split tail (below) from this many pixel groups on: linear scenes from
+    // PTG_TAIL_MIN_HALF_ROUNDS/2 rounds of the device's wave slots (then the
+    // head runs whole-pixel units even where ~96k units would split samples,
+    // e.g. an 8-GPU shard), BVH scenes only where whole-pixel units are the
+    // auto choice anyway
+    const long long tail_min =
+        ctx->n > kLinearMax ? PTG_BVH_UNIT_MULT * 98304LL : (long long)PTG_TAIL_MIN_HALF_ROUNDS * ctx->wave_slots / 2;
+    const bool tail_ok = p->chunk_samples <= 0 && !accumulate_only && s_begin == 0 && s_end == p->samples &&
+                         PTG_TAIL_CHUNKS > 1 && nsamp >= PTG_TAIL_CHUNKS && groups >= tail_min;
     int chunk = p->chunk_samples;
-    if (chunk <= 0) {
+    if (tail_ok) {
+        chunk = nsamp;
+    } else if (chunk <= 0) {
         const long long target = ctx->n > kLinearMax ? PTG_BVH_UNIT_MULT * 98304 : 98304;
         long long want = (target + groups - 1) / groups;
         long long nch = want < 1 ? 1 : (want > nsamp ? nsamp : want);
@@ -1277,9 +1310,9 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     // rows -- about one round of the device's wave slots -- run instead as
     // PTG_TAIL_CHUNKS shorter units each, accumulated and resolved by
     // resolve_kernel; everything before keeps the in-wave resolve.
-    if (A.single_chunk && p->chunk_samples <= 0 && PTG_TAIL_CHUNKS > 1 && nsamp >= PTG_TAIL_CHUNKS &&
-        groups >= 4 * ctx->wave_slots) {
-        const int tail_rows = (ctx->wave_slots + A.waves_per_row - 1) / A.waves_per_row;
+    if (tail_ok && A.single_chunk) {
+        int tail_rows = (ctx->wave_slots + A.waves_per_row - 1) / A.waves_per_row;
+        tail_rows = tail_rows < A.slab_rows ? tail_rows : A.slab_rows;
         A.tail_group = (A.slab_rows - tail_rows) * A.waves_per_row;
         A.n_head_chunks = 1;
         A.tail_chunk = (nsamp + PTG_TAIL_CHUNKS - 1) / PTG_TAIL_CHUNKS;
@@ -1404,10 +1437,26 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
         const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
-        const size_t total = off_q + n_nodes * sizeof(BvhNodeQ) + 16;
+        int shift = 0;  // layout stride: a power of two > n_nodes
+        while ((size_t(1) << shift) <= n_nodes)
+            ++shift;
+        const size_t stride = size_t(1) << shift, n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
+        const size_t total = off_q + n_layouts * stride * sizeof(BvhNodeQ) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
-        std::memcpy(blob.data() + off_q, qn.data(), n_nodes * sizeof(BvhNodeQ));
+        for (size_t k = 0; k < n_layouts; ++k) {
+            std::vector<BvhNodeQ> qk;
+            if (k == 0)
+                qk = qn;
+            else
+                quantise_bvh(order_bvh(b, (int)k), qk);  // same root box: same grid
+            for (BvhNodeQ &z : qk)
+                if (z.word >= 0)
+                    z.word += (int32_t)(k * stride);  // absolute skip index
+            std::memcpy(blob.data() + off_q + k * stride * sizeof(BvhNodeQ), qk.data(), n_nodes * sizeof(BvhNodeQ));
+        }
+        A.bvh_shift = shift;
+        A.bvh_mask = (int)(stride - 1);
         for (int c = 0; c < 3; ++c) {
             A.q_lo[c] = grid.lo[c];
             A.q_scale[c] = grid.scale[c];

@@ -32,6 +32,41 @@ static int fails = 0;
         }                                                                                          \
     } while (0)
 
+// depth-first skip layout, leaf coverage and box containment of one layout
+static void check_layout(const std::vector<ptg_sphere> &s, const BvhBuild &b, const std::vector<BvhNodeHost> &nodes,
+                         int octant)
+{
+    const int nn = (int)nodes.size();
+    CHECK(nn == (int)b.nodes.size(), "octant %d: %d nodes", octant, nn);
+    std::vector<int> leaf_cover(b.order.size(), 0);
+    for (int i = 0; i < nn; ++i) {
+        const BvhNodeHost &nd = nodes[i];
+        CHECK(nd.skip > i && nd.skip <= nn, "octant %d node %d skip %d", octant, i, nd.skip);
+        if (nd.leaf >= 0) {
+            CHECK(nd.skip == i + 1, "octant %d leaf %d skip %d", octant, i, nd.skip);
+            const int first = nd.leaf & 0xFFFFFF, cnt = nd.leaf >> 24;
+            CHECK(cnt >= 1 && cnt <= kLeafSize && first + cnt <= (int)b.order.size(), "leaf %d range", i);
+            for (int k = first; k < first + cnt; ++k) {
+                leaf_cover[k] += 1;
+                const ptg_sphere &sp = s[b.order[k]];
+                for (int c = 0; c < 3; ++c)
+                    CHECK(nd.bmin[c] <= sp.position[c] - sp.radius && nd.bmax[c] >= sp.position[c] + sp.radius,
+                          "octant %d leaf %d does not contain sphere %d (axis %d)", octant, i, b.order[k], c);
+            }
+        } else {
+            CHECK(i + 1 < nd.skip, "octant %d inner node %d has no children", octant, i);
+            const int l = i + 1, r = nodes[l].skip;
+            CHECK(r < nd.skip && nodes[r].skip == nd.skip, "octant %d inner node %d children %d %d", octant, i, l, r);
+            for (int ch : {l, r})
+                for (int c = 0; c < 3; ++c)
+                    CHECK(nd.bmin[c] <= nodes[ch].bmin[c] && nd.bmax[c] >= nodes[ch].bmax[c],
+                          "octant %d node %d does not contain child %d", octant, i, ch);
+        }
+    }
+    for (size_t k = 0; k < leaf_cover.size(); ++k)
+        CHECK(leaf_cover[k] == 1, "octant %d leaf slot %zu covered %d times", octant, k, leaf_cover[k]);
+}
+
 static void check_scene(const std::vector<ptg_sphere> &s)
 {
     const int n = (int)s.size();
@@ -46,34 +81,25 @@ static void check_scene(const std::vector<ptg_sphere> &s)
         CHECK(seen[i] == (huge ? 1 : 10), "sphere %d placed %d (huge %d)", i, seen[i], (int)huge);
     }
     const int nn = (int)b.nodes.size();
-    // subtree ranges and containment
-    std::vector<int> leaf_cover(b.order.size(), 0);
-    for (int i = 0; i < nn; ++i) {
-        const BvhNodeHost &nd = b.nodes[i];
-        CHECK(nd.skip > i && nd.skip <= nn, "node %d skip %d", i, nd.skip);
-        if (nd.leaf >= 0) {
-            CHECK(nd.skip == i + 1, "leaf %d skip %d", i, nd.skip);
-            const int first = nd.leaf & 0xFFFFFF, cnt = nd.leaf >> 24;
-            CHECK(cnt >= 1 && cnt <= kLeafSize && first + cnt <= (int)b.order.size(), "leaf %d range", i);
-            for (int k = first; k < first + cnt; ++k) {
-                leaf_cover[k] += 1;
-                const ptg_sphere &sp = s[b.order[k]];
-                for (int c = 0; c < 3; ++c)
-                    CHECK(nd.bmin[c] <= sp.position[c] - sp.radius && nd.bmax[c] >= sp.position[c] + sp.radius,
-                          "leaf %d does not contain sphere %d (axis %d)", i, b.order[k], c);
-            }
-        } else {
-            CHECK(i + 1 < nd.skip, "inner node %d has no children", i);
-            const int l = i + 1, r = b.nodes[l].skip;
-            CHECK(r < nd.skip && b.nodes[r].skip == nd.skip, "inner node %d children %d %d", i, l, r);
-            for (int ch : {l, r})
-                for (int c = 0; c < 3; ++c)
-                    CHECK(nd.bmin[c] <= b.nodes[ch].bmin[c] && nd.bmax[c] >= b.nodes[ch].bmax[c],
-                          "node %d does not contain child %d", i, ch);
+    CHECK((int)b.axis.size() == nn, "axis per node");
+    check_layout(s, b, b.nodes, 0);
+    // the 8 octant layouts (ptg_render.hip: one per ray-direction octant):
+    // octant 0 is the build order; in octant k every inner node whose split
+    // axis has bit k set lists its high-side child first
+    for (int oct = 0; oct < 8 && !fails; ++oct) {
+        const std::vector<BvhNodeHost> lay = order_bvh(b, oct);
+        check_layout(s, b, lay, oct);
+        if (oct == 0)
+            for (int i = 0; i < nn; ++i)
+                CHECK(lay[i].skip == b.nodes[i].skip && lay[i].leaf == b.nodes[i].leaf, "octant 0 node %d", i);
+        if (!fails && nn > 1 && lay[0].leaf < 0) {
+            const int first_child = b.axis[0] >= 0 && ((oct >> b.axis[0]) & 1) ? b.nodes[1].skip : 1;
+            CHECK(lay[1].leaf == b.nodes[first_child].leaf && lay[1].bmin[0] == b.nodes[first_child].bmin[0],
+                  "octant %d: root's first child", oct);
         }
     }
-    for (size_t k = 0; k < leaf_cover.size(); ++k)
-        CHECK(leaf_cover[k] == 1, "leaf slot %zu covered %d times", k, leaf_cover[k]);
+    if (fails)
+        return;
     // quantised boxes contain the float boxes
     std::vector<BvhNodeQ> q;
     const BvhGrid g = quantise_bvh(b.nodes, q);
@@ -94,7 +120,7 @@ static void check_scene(const std::vector<ptg_sphere> &s)
         else
             CHECK(z.word == nd.skip, "quantised skip %d", i);
     }
-    std::printf("ok %d spheres %d nodes %zu huge\n", n, nn, b.big.size());
+    std::printf("ok %d spheres %d nodes %zu huge, 8 octant layouts\n", n, nn, b.big.size());
 }
 
 int main()

@@ -343,3 +343,30 @@ def test_split_tail_frame_is_exact():
     for y in (0, 1, 2, 537, H - 1):  # y = 0.. are the bottom image rows = the last slab rows (the tail)
         ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
         _check_equal(tail[H - 1 - y], ref[H - 1 - y])
+
+
+def test_shards_with_split_tail_are_exact():
+    """2-, 4- and 8-way shards of a full-size frame run whole-pixel units with
+    a split tail (fill_launch: from 1.5 rounds of wave slots on); gathered,
+    they equal the 1-GPU frame bit for bit, and rows of the last slab rows
+    (the split tail of each shard) equal the oracle."""
+    _require_gpu()
+    W, H, samps = 1920, 1080, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    full, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    sp, ca = _oracle_scene(scn, cam)
+    with ptgpu.Context(scn, cam) as ctx:
+        for count in (2, 4, 8):
+            rows = ptgpu.shard_rows(H, 1, count)
+            gathered = torch.zeros((count, rows * W * 3), dtype=torch.float32, device="cuda")
+            for k in range(count):
+                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count))
+            image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+            ptgpu.unshard_device(gathered, image, W, H, 1, count)
+            torch.cuda.synchronize()
+            assert np.array_equal(image.cpu().numpy(), full), count
+    # image row H-1-y sits in slab row (H-1-y) // count: y = 0, 1 are in the last slab rows
+    for y in (0, 1, H - 1):
+        ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
+        _check_equal(full[H - 1 - y], ref[H - 1 - y])
