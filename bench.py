@@ -115,8 +115,9 @@ def load_pmc(workload):
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
+        if d.get("workload") == workload:  # single-record file
             return d
+        return d.get(workload, {})
     except (OSError, ValueError):
         pass
     return {}

@@ -83,7 +83,7 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #define PTG_LEAF_FRAC 6  // BVH: leaf phase once 6/8 of the walking lanes hold a leaf (measured: 6 beats 4 by 2 %)
 #endif
 #ifndef PTG_BVH_UNIT_MULT
-#define PTG_BVH_UNIT_MULT 4  // BVH scenes: aim at this many times more work units
+#define PTG_BVH_UNIT_MULT 2  // BVH scenes below the split-tail threshold: this many times more work units (8-way C5 shards: 2 beats 1 and 4 by 2-5 %)
 #endif
 #ifndef PTG_TAIL_CHUNKS
 #define PTG_TAIL_CHUNKS 8  // split-tail units per pixel group of the last rows (1: off)
@@ -96,6 +96,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #endif
 #ifndef PTG_BVH_OCTANTS
 #define PTG_BVH_OCTANTS 1  // BVH: one depth-first layout per ray-direction octant (near child first)
+#endif
+#ifndef PTG_BVH_TAIL_MIN_HALF_ROUNDS
+#define PTG_BVH_TAIL_MIN_HALF_ROUNDS 6  // BVH scenes: split tail from 3 rounds of wave slots on
 #endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
@@ -1271,18 +1274,20 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
-    // BVH scenes aim at 4x as many: their cost varies strongly over the image
-    // (10,000-sphere scene: sky rows vs the sphere field), and shorter units
-    // shorten the tail of expensive rows (measured: 64-sample units 551 ms vs
-    // 573 ms for whole-pixel units; on box_scene whole-pixel units are best).
+    // Below the split-tail threshold, BVH scenes aim at PTG_BVH_UNIT_MULT
+    // times more units: their cost varies strongly over the image (sky rows
+    // vs the sphere field).
     const int groups = A.slab_rows * A.waves_per_row;
-    // split tail (below) from this many pixel groups on: linear scenes from
-    // PTG_TAIL_MIN_HALF_ROUNDS/2 rounds of the device's wave slots (then the
-    // head runs whole-pixel units even where ~96k units would split samples,
-    // e.g. an 8-GPU shard), BVH scenes only where whole-pixel units are the
-    // auto choice anyway
-    const long long tail_min =
-        ctx->n > kLinearMax ? PTG_BVH_UNIT_MULT * 98304LL : (long long)PTG_TAIL_MIN_HALF_ROUNDS * ctx->wave_slots / 2;
+    // split tail (below) from PTG_TAIL_MIN_HALF_ROUNDS/2 rounds of the
+    // device's wave slots on, BVH scenes from PTG_BVH_TAIL_MIN_HALF_ROUNDS/2
+    // (then the head runs whole-pixel units even where ~96k units would split
+    // samples, e.g. an 8-GPU shard).  The head's units are whole pixels, so
+    // the head needs enough rounds to average out the rows' different costs:
+    // at 2 rounds (8-way shards of the bench frame) the split tail gains
+    // 1.7-2.1 % on the box scenes but loses 28 % on the 10,000-sphere scene
+    // (tools/scene_shard_ab.sh); from 4 rounds on it gains on both.
+    const long long tail_min = (long long)(ctx->n > kLinearMax ? PTG_BVH_TAIL_MIN_HALF_ROUNDS : PTG_TAIL_MIN_HALF_ROUNDS) *
+                               ctx->wave_slots / 2;
     const bool tail_ok = p->chunk_samples <= 0 && !accumulate_only && s_begin == 0 && s_end == p->samples &&
                          PTG_TAIL_CHUNKS > 1 && nsamp >= PTG_TAIL_CHUNKS && groups >= tail_min;
     int chunk = p->chunk_samples;

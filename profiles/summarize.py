@@ -86,8 +86,18 @@ def main(src, tag, kernel_sub="render_kernel"):
         rec["clock_GHz"] = round(out["derived"]["clock_GHz"], 3)
     if "valu_insts_per_segment_wave_level" in out:
         rec["valu_insts_per_64_lane_segments"] = round(out["valu_insts_per_segment_wave_level"], 1)
-    with open(os.path.join(os.path.dirname(dst), "pmc_traffic.json"), "w") as f:
-        json.dump(rec, f)
+    # one record per workload (bench.py load_pmc looks its workload up)
+    pt = os.path.join(os.path.dirname(dst), "pmc_traffic.json")
+    try:
+        with open(pt) as f:
+            allrec = json.load(f)
+    except (OSError, ValueError):
+        allrec = {}
+    if "workload" in allrec:  # older single-record file
+        allrec = {allrec["workload"]: allrec}
+    allrec[rec["workload"]] = rec
+    with open(pt, "w") as f:
+        json.dump(allrec, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])
 
 
