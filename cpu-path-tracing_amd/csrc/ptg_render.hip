@@ -110,7 +110,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
-constexpr int kWavesPerBlock = kBlock / 64;
+#ifndef PTG_BVH_BLOCK
+#define PTG_BVH_BLOCK 64  // BVH render kernel: one wave per workgroup, so a wave slot frees as soon as its unit ends
+                          // (units of the 10,000-sphere scene differ widely in length: 64 beats 256 by 10 %, 128 by 6 %)
+#endif
+template <bool kBvh>
+constexpr int kBlockOf = kBvh ? PTG_BVH_BLOCK : kBlock;
 constexpr double kBigRadius = 1000.0;
 
 struct KArgs {
@@ -613,11 +618,12 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
 template <bool kCount, bool kBvh>
-__global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
+__global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
-    __shared__ unsigned long long lds_acc[kWavesPerBlock][64 * 3];
-    __shared__ unsigned long long lds_key[kWavesPerBlock][64];
-    __shared__ uint32_t lds_pix[kWavesPerBlock][64];  // slot -> x | sx << 20 | sy << 26
+    constexpr int kWaves = kBlockOf<kBvh> / 64;
+    __shared__ unsigned long long lds_acc[kWaves][64 * 3];
+    __shared__ unsigned long long lds_key[kWaves][64];
+    __shared__ uint32_t lds_pix[kWaves][64];  // slot -> x | sx << 20 | sy << 26
     // sphere records staged once per workgroup in LDS (uniform-address
     // ds_read_b128 broadcasts in the scan, by-id gathers at hits); larger
     // scenes read geometry with wave-uniform scalar loads from L2/HBM instead
@@ -645,7 +651,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     // wave-uniform by construction; readfirstlane lets the compiler keep all
     // per-unit bookkeeping in SGPRs
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const long long unit = (long long)blockIdx.x * kWavesPerBlock + wv;
+    const long long unit = (long long)blockIdx.x * kWaves + wv;
     if (unit >= A.n_units)
         return;  // whole wave
     // head units: groups [0, tail_group) x n_head_chunks chunks of A.chunk
@@ -705,7 +711,7 @@ __global__ __launch_bounds__(kBlock, PTG_MIN_WAVES_PER_EU) void render_kernel(KA
     // whose path ends starts the prefetched one at once (two LDS reads), and
     // the camera code runs only in refills of >= PTG_REFILL_BATCH lanes (or
     // when a lane would otherwise idle).
-    __shared__ float4 lds_pre[kWavesPerBlock][64][2];
+    __shared__ float4 lds_pre[kWaves][64][2];
     auto ray_of = [&](int it, f3 &ro, f3 &rd, uint32_t &rs) {
         int sl, sample;
         if (nv == 64) {
@@ -1326,7 +1332,8 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
         A.resolve_row0 = A.slab_rows - tail_rows;
         A.n_units = (long long)A.tail_group + (long long)(groups - A.tail_group) * tail_chunks;
     }
-    grid = (int)((A.n_units + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int waves_per_block = (ctx->n > kLinearMax ? PTG_BVH_BLOCK : kBlock) / 64;
+    grid = (int)((A.n_units + waves_per_block - 1) / waves_per_block);
 }
 
 int set_device(int device)
@@ -1582,9 +1589,11 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     const bool bvh = A.n > kLinearMax;
     const size_t lds = bvh ? 0 : (size_t)(A.n + 1) * sizeof(LinRec);
     if (count)
-        bvh ? render_kernel<true, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<true, false><<<grid, kBlock, lds, s>>>(A);
+        bvh ? render_kernel<true, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A)
+            : render_kernel<true, false><<<grid, kBlock, lds, s>>>(A);
     else
-        bvh ? render_kernel<false, true><<<grid, kBlock, 0, s>>>(A) : render_kernel<false, false><<<grid, kBlock, lds, s>>>(A);
+        bvh ? render_kernel<false, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A)
+            : render_kernel<false, false><<<grid, kBlock, lds, s>>>(A);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }
