@@ -59,7 +59,14 @@ int fail(int code, const std::string &msg)
         }                                                                                          \
     } while (0)
 
-constexpr int kBlock = 256;        // 4 waves per workgroup
+#ifndef PTG_BLOCK
+#define PTG_BLOCK 256  // linear-scene render kernel workgroup size
+#endif
+#ifndef PTG_TRIG_LDS
+#define PTG_TRIG_LDS 1  // linear-scene render kernel: sin/cos table in LDS (0: read through L1)
+#endif
+constexpr int kBlock = PTG_BLOCK;
+constexpr int kTraceBlock = 256;  // parity probe kernel
 #ifndef PTG_MAX_LDS_SPHERES
 #define PTG_MAX_LDS_SPHERES 64
 #endif
@@ -637,11 +644,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     // on its node loads) reads it from global memory (L1): measured the same
     const float2 *trig = A.trig;
     if constexpr (kLdsGeo) {
+#if PTG_TRIG_LDS
         __shared__ float2 lds_trig[kTrigEntries];
-        static_assert(kTrigEntries <= kBlock, "one table entry per thread");
-        if (threadIdx.x < kTrigEntries)
-            lds_trig[threadIdx.x] = A.trig[threadIdx.x];
+        for (int i = threadIdx.x; i < kTrigEntries; i += kBlock)
+            lds_trig[i] = A.trig[i];
         trig = lds_trig;
+#endif
         for (int i = threadIdx.x; i <= A.n; i += kBlock)  // n records + the sentinel
             lds_lin[i] = A.lin[i];
         recs = lds_lin;
@@ -991,10 +999,10 @@ __global__ __launch_bounds__(256) void resolve_kernel(KArgs A)
 
 // Parity probe: one path per record {x, y, sx, sy, sample}.
 template <bool kBvh>
-__global__ __launch_bounds__(kBlock) void trace_kernel(KArgs A, const int32_t *coords, int n, float *out,
+__global__ __launch_bounds__(kTraceBlock) void trace_kernel(KArgs A, const int32_t *coords, int n, float *out,
                                                          int32_t *segs_out)
 {
-    int i = blockIdx.x * kBlock + threadIdx.x;
+    int i = blockIdx.x * kTraceBlock + threadIdx.x;
     if (i >= n)
         return;
     Lane L;
@@ -1714,11 +1722,11 @@ int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const i
     int grid = 0;
     fill_launch(ctx, params, A, grid);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    int blocks = (int)((n + kBlock - 1) / kBlock);
+    int blocks = (int)((n + kTraceBlock - 1) / kTraceBlock);
     if (A.n > kLinearMax)
-        trace_kernel<true><<<blocks, kBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+        trace_kernel<true><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
     else
-        trace_kernel<false><<<blocks, kBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+        trace_kernel<false><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }
