@@ -135,6 +135,12 @@ struct KArgs {
     // then the small spheres up to n
     int end_ax[3];
     int end_big;
+    // wall pairs (pair_walls): axis k's group starts with a pair when
+    // pairs[k] = 1 -- its wall on the + side, then its wall on the - side; a
+    // lane whose origin lies in [pair_lo[k], pair_hi[k]] tests only the wall
+    // its direction moves toward (d_k >= 0: the + wall)
+    int pairs[3];
+    float pair_lo[3], pair_hi[3];
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
     const uint4 *bvh_qnodes;  // the same nodes, compact (bvh_build.hpp BvhNodeQ; render kernel)
@@ -239,7 +245,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     const LinRec *best = recs + A.n;
     auto test = [&](const int i, auto kind_tag) {
         constexpr int kKind = decltype(kind_tag)::value;
-        const LinRec *r = recs + i;
+        const LinRec *r = recs + i;  // wave-uniform, except for a pair's walls
         float4 g0 = r->g.g0;
         float4 g1 = r->g.g1;
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
@@ -275,12 +281,29 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     // scan order: axis-anchored walls (x, y, z), general huge spheres, small
     // spheres (host: prepare_scan_order)
     int i = 0;
-    for (; i < A.end_ax[0]; ++i)
-        test(i, std::integral_constant<int, kAxX>{});
-    for (; i < A.end_ax[1]; ++i)
-        test(i, std::integral_constant<int, kAxY>{});
-    for (; i < A.end_ax[2]; ++i)
-        test(i, std::integral_constant<int, kAxZ>{});
+    // a wall pair: the + wall at i, the - wall at i + 1.  A ray whose origin
+    // is on the room side of both walls' tangent planes (within a margin) can
+    // only hit the wall it moves toward (DESIGN.md "wall pairs"); other lanes
+    // (origins outside the room, rare) test both, the one moved toward first
+    auto axis_group = [&](auto kind_tag) {
+        constexpr int k = decltype(kind_tag)::value;
+        if (A.pairs[k]) {
+            const bool pos = comp(d, k) >= 0.0f;
+            test(pos ? i : i + 1, kind_tag);
+            const float ok = comp(o, k);
+            const bool outside = !(ok >= A.pair_lo[k]) | !(ok <= A.pair_hi[k]);
+            if (__ballot(outside) != 0ull) {
+                if (outside)
+                    test(pos ? i + 1 : i, kind_tag);
+            }
+            i += 2;
+        }
+        for (; i < A.end_ax[k]; ++i)
+            test(i, kind_tag);
+    };
+    axis_group(std::integral_constant<int, kAxX>{});
+    axis_group(std::integral_constant<int, kAxY>{});
+    axis_group(std::integral_constant<int, kAxZ>{});
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
     for (; i < A.n; ++i)
@@ -1196,15 +1219,62 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
     }
 }
 
-// Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z,
-// then the other huge spheres, then the small ones, each group in scene index
-// order; end_ax / end_big receive the group ends.
-std::vector<int> scan_order_of(const ptg_sphere *s, int n, const std::vector<int> &axis, KArgs &A)
+// Wall pairs (DESIGN.md "wall pairs"): on each axis k, the first (scene
+// index order) axis-anchored huge sphere whose centre lies on the + side of
+// its anchor (anchor normal -e_k) and the first one on the - side.  Their
+// tangent planes at the anchors, x_k = a_plus and x_k = a_minus, bound the
+// room: a ray from an origin with a_minus <= o_k <= a_plus can hit the + wall
+// only if d_k > 0 and the - wall only if d_k < 0 (each sphere lies entirely
+// beyond its tangent plane).  The bounds widen by a margin of 1e-4 max(1, box
+// diagonal) so that rays leaving a wall (origin rounded a hair past its
+// plane) keep the rule; pair_lo/hi are those bounds rounded to float.  The
+// oracle's prep_B forms the same pairs (pt_oracle.c).  plus[k] / minus[k] =
+// scene index or -1.
+void pair_walls(const ptg_sphere *s, int n, const std::vector<int> &axis, const std::vector<GeoRec> &geo,
+                const SceneBox &box, int plus[3], int minus[3], float lo[3], float hi[3])
+{
+    const double margin = 1e-4 * std::max(1.0, box.diag);
+    for (int k = 0; k < 3; ++k) {
+        plus[k] = minus[k] = -1;
+        for (int i = 0; i < n; ++i) {
+            if (axis[i] != k)
+                continue;
+            const float nk = (&geo[i].g1.x)[k];  // anchor normal component: exactly +-1
+            if (nk < 0.0f && plus[k] < 0)
+                plus[k] = i;
+            if (nk > 0.0f && minus[k] < 0)
+                minus[k] = i;
+        }
+        if (plus[k] < 0 || minus[k] < 0) {
+            plus[k] = minus[k] = -1;
+            lo[k] = hi[k] = 0.0f;
+            continue;
+        }
+        const double a_plus = s[plus[k]].position[k] - s[plus[k]].radius;
+        const double a_minus = s[minus[k]].position[k] + s[minus[k]].radius;
+        lo[k] = (float)(a_minus - margin);
+        hi[k] = (float)(a_plus + margin);
+    }
+}
+
+// Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z
+// (each axis group led by its wall pair, + wall first), then the other huge
+// spheres, then the small ones, each group otherwise in scene index order;
+// end_ax / end_big / pairs receive the group ends and pair flags.
+std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
+                               const std::vector<GeoRec> &geo, KArgs &A)
 {
     std::vector<int> order;
+    int plus[3], minus[3];
+    pair_walls(s, n, axis, geo, scene_box(s, n, cam), plus, minus, A.pair_lo, A.pair_hi);
     for (int k = 0; k < 3; ++k) {
+        A.pairs[k] = plus[k] >= 0 ? 1 : 0;
+        if (A.pairs[k]) {
+            order.push_back(plus[k]);
+            order.push_back(minus[k]);
+        }
         for (int i = 0; i < n; ++i)
-            if (axis[i] == k)
+            if (axis[i] == k && i != plus[k] && i != minus[k])
                 order.push_back(i);
         A.end_ax[k] = (int)order.size();
     }
@@ -1220,13 +1290,13 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const std::vector<int
 
 // Records in scan order.  Axis-anchored records carry the signs in their
 // constants: g0.w = s R, g1.w = s 2R (the kernel reads e_k and d_k).
-void prepare_scan_order(const ptg_sphere *s, int n, const std::vector<GeoRec> &geo,
+void prepare_scan_order(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<GeoRec> &geo,
                         const std::vector<ShadeRec> &shade, const std::vector<int> &axis,
                         std::vector<GeoRec> &lgeo, std::vector<ShadeRec> &lshade, KArgs &A)
 {
     lgeo.clear();
     lshade.clear();
-    for (int i : scan_order_of(s, n, axis, A)) {
+    for (int i : scan_order_of(s, n, cam, axis, geo, A)) {
         GeoRec g = geo[i];
         if (axis[i] >= 0) {
             const float sgn = (&g.g1.x)[axis[i]];  // +-1 exactly
@@ -1407,7 +1477,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     const bool linear = (int)n_spheres <= kLinearMax;
     std::vector<LinRec> lin;
     if (linear) {  // the scan's record order, interleaved, + the no-hit sentinel
-        prepare_scan_order(spheres, (int)n_spheres, geo, shade, axis, lgeo, lshade, order);
+        prepare_scan_order(spheres, (int)n_spheres, cam, geo, shade, axis, lgeo, lshade, order);
         lin.resize(n_spheres + 1);
         std::memset(lin.data(), 0, lin.size() * sizeof(LinRec));
         for (size_t i = 0; i < n_spheres; ++i)
@@ -1445,8 +1515,12 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.lin = ctx->d_lin;
     A.shade = ctx->d_shade;
     A.n = (int)n_spheres;
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < 3; ++k) {
         A.end_ax[k] = order.end_ax[k];
+        A.pairs[k] = order.pairs[k];
+        A.pair_lo[k] = order.pair_lo[k];
+        A.pair_hi[k] = order.pair_hi[k];
+    }
     A.end_big = order.end_big;
     if ((int)n_spheres > kLinearMax) {
         BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);
@@ -1537,12 +1611,15 @@ int ptg_scene_layout(const ptg_sphere *spheres, size_t n_spheres, const ptg_came
     std::vector<ShadeRec> shade;
     std::vector<int> axis;
     prepare_scene(spheres, n, cam, geo, shade, axis);
-    for (int i = 0; i < n; ++i)
-        anchor_axis[i] = axis[i];
     KArgs ends{};
     std::vector<int> order;
     if (n <= kLinearMax)
-        order = scan_order_of(spheres, n, axis, ends);
+        order = scan_order_of(spheres, n, cam, axis, geo, ends);
+    for (int i = 0; i < n; ++i)
+        anchor_axis[i] = axis[i];
+    for (int k = 0; k < 3 && n <= kLinearMax; ++k)
+        if (ends.pairs[k])  // the pair leads axis k's group
+            anchor_axis[order[k == 0 ? 0 : ends.end_ax[k - 1]]] = anchor_axis[order[(k == 0 ? 0 : ends.end_ax[k - 1]) + 1]] = k + 3;
     for (int i = 0; i < n; ++i)
         scan_order[i] = n <= kLinearMax ? order[i] : i;
     return PTG_OK;

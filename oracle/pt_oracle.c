@@ -606,6 +606,8 @@ typedef struct {
     int mat;
     int axis;         /* huge sphere anchored on axis 0..2, else -1 (choose_anchor_B) */
     int visit;        /* linear scan: the sphere visited at scan position (this element's index) */
+    int pair;         /* wall pair member (pair_walls_B): +1 the + wall, -1 the - wall, 0 none */
+    float plo, phi;   /* on the + wall: the pair's origin bounds */
 } sphB;
 
 typedef struct {
@@ -676,6 +678,36 @@ static boxB scene_box_B(const po_sphere *s, int n, const po_camera *cam)
 
 static void trig_table_B(float *tab);
 
+/* Wall pairs (DESIGN.md "wall pairs"; the kernel's host side:
+ * ptg_render.hip pair_walls): on each axis k the first axis-anchored huge
+ * sphere with its centre on the + side of its anchor (N = -e_k) and the first
+ * on the - side.  A ray whose origin has pair_lo <= o_k <= pair_hi (the
+ * tangent planes x_k = a_minus, a_plus widened by 1e-4 max(1, diagonal)) tests
+ * only the wall it moves toward (d_k >= 0: the + wall): each sphere lies
+ * entirely beyond its tangent plane. */
+static void pair_walls_B(const po_sphere *s, int n, const boxB *box, sphB *out)
+{
+    const double margin = 1e-4 * (box->diag > 1.0 ? box->diag : 1.0);
+    for (int k = 0; k < 3; ++k) {
+        int plus = -1, minus = -1;
+        for (int i = 0; i < n; ++i) {
+            if (!out[i].big || out[i].axis != k)
+                continue;
+            const float nk = k == 0 ? out[i].N.x : (k == 1 ? out[i].N.y : out[i].N.z);
+            if (nk < 0.0f && plus < 0)
+                plus = i;
+            if (nk > 0.0f && minus < 0)
+                minus = i;
+        }
+        if (plus < 0 || minus < 0)
+            continue;
+        out[plus].pair = 1;
+        out[minus].pair = -1;
+        out[plus].plo = (float)(s[minus].position[k] + s[minus].radius - margin);
+        out[plus].phi = (float)(s[plus].position[k] - s[plus].radius + margin);
+    }
+}
+
 static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
 {
     boxB box = scene_box_B(s, n, cam);
@@ -689,6 +721,8 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         b->negR2 = (float)(-(R * R));
         b->invR = (float)(1.0 / R);
         b->axis = -1;
+        b->pair = 0;
+        b->plo = b->phi = 0.0f;
         if (b->big) {
             double P[3], N[3];
             b->axis = choose_anchor_B(sp, cam, &box, P, N);
@@ -714,14 +748,23 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         b->mat = sp->material;
     }
     /* linear scan order (the kernel's record order, ptg_render.hip
-     * prepare_scan_order): x-, y-, z-axis-anchored huge spheres, the other
-     * huge spheres, the small ones; each group in index order */
+     * prepare_scan_order): x-, y-, z-axis-anchored huge spheres (each axis
+     * led by its wall pair, + wall first), the other huge spheres, the small
+     * ones; each group otherwise in index order */
     if (n <= LINEAR_MAX_PREP) {
+        pair_walls_B(s, n, &box, out);
         int j = 0;
-        for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < 3; ++k) {
             for (int i = 0; i < n; ++i)
-                if (out[i].big && out[i].axis == k)
+                if (out[i].big && out[i].axis == k && out[i].pair == 1)
                     out[j++].visit = i;
+            for (int i = 0; i < n; ++i)
+                if (out[i].big && out[i].axis == k && out[i].pair == -1)
+                    out[j++].visit = i;
+            for (int i = 0; i < n; ++i)
+                if (out[i].big && out[i].axis == k && out[i].pair == 0)
+                    out[j++].visit = i;
+        }
         for (int i = 0; i < n; ++i)
             if (out[i].big && out[i].axis < 0)
                 out[j++].visit = i;
@@ -797,6 +840,53 @@ static void trig_table_B(float *tab)
  * (hb < 0 only) q/a.  Two exact culls skip spheres that provably cannot win
  * (they never change the result: DESIGN.md "scene scan"). */
 #define CULL_MARGIN 0x1.00001p+0f /* 1 + 2^-20 */
+/* one candidate: the nearest root >= eps of sphere i, if nearer than bn/bq */
+static void test_B(const sphB *sp, int i, f3 o, f3 d, float a, float *bn, float *bq, int *id)
+{
+    f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
+    float ed = fdot(e, d);
+    float ee = fdot(e, e);
+    float hb, c;
+    if (sp->big) {
+        hb = fmaf(sp->R, fdot(sp->N, d), ed);
+        c = fmaf(sp->R2x, fdot(e, sp->N), ee);
+    } else {
+        hb = ed;
+        c = ee + sp->negR2;
+    }
+    if (hb >= 0.0f && c >= 0.0f)
+        return; /* both roots <= 0 */
+    if (hb < 0.0f && c > 0.0f && c * *bq >= (*bn * (-2.0f * hb)) * CULL_MARGIN)
+        return; /* near root provably not nearer than bn/bq */
+    float disc = fmaf(hb, hb, -(a * c));
+    if (disc < 0.0f)
+        return;
+    float sq = sqrt_gs_B(disc); /* disc >= 0 here */
+    float num, den;
+    if (hb < 0.0f) {
+        float q = sq - hb; /* > 0; roots c/q (near) and q/a (far) */
+        num = c;
+        den = q;
+        if (c < EPSF * q) { /* near root < eps */
+            num = q;
+            den = a;
+            if (q < EPSF * a)
+                return;
+        }
+    } else {
+        float qn = hb + sq; /* > 0 here (c < 0): root c/-qn */
+        num = -c;
+        den = qn;
+        if (num < EPSF * den)
+            return;
+    }
+    if (num * *bq < *bn * den) {
+        *bn = num;
+        *bq = den;
+        *id = i;
+    }
+}
+
 static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
 {
     /* nearest root kept as a fraction bn/bq (bq > 0): candidates are compared
@@ -806,49 +896,17 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
     int id = -1;
     for (int j = 0; j < n; ++j) {
         const int i = s[j].visit; /* scan order: first visited wins exact ties */
-        const sphB *sp = &s[i];
-        f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
-        float ed = fdot(e, d);
-        float ee = fdot(e, e);
-        float hb, c;
-        if (sp->big) {
-            hb = fmaf(sp->R, fdot(sp->N, d), ed);
-            c = fmaf(sp->R2x, fdot(e, sp->N), ee);
-        } else {
-            hb = ed;
-            c = ee + sp->negR2;
-        }
-        if (hb >= 0.0f && c >= 0.0f)
-            continue; /* both roots <= 0 */
-        if (hb < 0.0f && c > 0.0f && c * bq >= (bn * (-2.0f * hb)) * CULL_MARGIN)
-            continue; /* near root provably not nearer than bn/bq */
-        float disc = fmaf(hb, hb, -(a * c));
-        if (disc < 0.0f)
+        if (s[i].pair == 1) { /* wall pair: + wall at j, - wall at j + 1 */
+            const int im = s[j + 1].visit, k = s[i].axis;
+            const float dk = k == 0 ? d.x : (k == 1 ? d.y : d.z), ok = k == 0 ? o.x : (k == 1 ? o.y : o.z);
+            const int first = dk >= 0.0f ? i : im, second = dk >= 0.0f ? im : i;
+            test_B(&s[first], first, o, d, a, &bn, &bq, &id);
+            if (!(ok >= s[i].plo) || !(ok <= s[i].phi)) /* origin outside the room: both */
+                test_B(&s[second], second, o, d, a, &bn, &bq, &id);
+            j += 1;
             continue;
-        float sq = sqrt_gs_B(disc); /* disc >= 0 here */
-        float num, den;
-        if (hb < 0.0f) {
-            float q = sq - hb; /* > 0; roots c/q (near) and q/a (far) */
-            num = c;
-            den = q;
-            if (c < EPSF * q) { /* near root < eps */
-                num = q;
-                den = a;
-                if (q < EPSF * a)
-                    continue;
-            }
-        } else {
-            float qn = hb + sq; /* > 0 here (c < 0): root c/-qn */
-            num = -c;
-            den = qn;
-            if (num < EPSF * den)
-                continue;
         }
-        if (num * bq < bn * den) {
-            bn = num;
-            bq = den;
-            id = i;
-        }
+        test_B(&s[i], i, o, d, a, &bn, &bq, &id);
     }
     *tout = id >= 0 ? div_B(bn, bq) : INFF;
     *idout = id;
@@ -1119,7 +1177,7 @@ int po_scan_layout(const po_sphere *s, int n, const po_camera *cam, int32_t *axi
     camB cb;
     prep_B(s, n, cam, sb, &cb);
     for (int i = 0; i < n; ++i) {
-        axis[i] = sb[i].axis;
+        axis[i] = sb[i].pair != 0 ? sb[i].axis + 3 : sb[i].axis; /* 3..5: paired wall */
         order[i] = sb[i].visit;
     }
     free(sb);

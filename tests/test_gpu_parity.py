@@ -116,7 +116,25 @@ def test_tilted_huge_spheres_take_the_general_anchor():
     ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
     _check_equal(gpu, ref)
     assert gsegs == rsegs
-    assert po.anchor_axes(sp, ca) == [-1, -1, -1, -1, 0, 0, 2, 1, 1]
+    # x and y walls form wall pairs (3 + axis); the back wall (z) is unpaired
+    assert po.anchor_axes(sp, ca) == [-1, -1, -1, -1, 3, 3, 2, 4, 4]
+
+
+@pytest.mark.parametrize("cam_pos", [(0.6, 0.0, 2.0), (0.0, -0.55, 0.3), (0.3, 0.2, 40.0)])
+def test_wall_pairs_with_origins_outside_the_room(cam_pos):
+    """Wall pairs: a lane whose origin lies outside the room (here the camera
+    beyond the right wall, below the floor, or far in front of the open box)
+    tests both walls of a pair; the image stays bit-exact with the oracle."""
+    _require_gpu()
+    W, H, samps = 48, 32, 8
+    scn = ptgpu.make_scene("box", W, H)
+    scn.camera_parameters.position = cam_pos
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    gpu, gsegs = _gpu_image(scn, cam, W, H, samps, count_segments=True)
+    sp, ca = _oracle_scene(scn, cam)
+    ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
+    _check_equal(gpu, ref)
+    assert gsegs == rsegs
 
 
 @pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:3000"])

@@ -131,10 +131,13 @@ def test_scene_layout_matches_oracle(name):
     ca = cam.to_array().view(po.CAMERA_DT)
     assert (axis, order) == po.scan_layout(sp, ca)
     assert sorted(order) == list(range(len(scn.spheres)))
+    # axis-anchored walls report their axis, wall pairs 3 + axis (+ wall first
+    # in the scan: right before left, ceiling before floor); the back wall
+    # has no partner
     if name in ("box", "box_mirror"):
-        assert axis == [0, 0, 2, 1, 1, -1, -1, -1] and order == [0, 1, 3, 4, 2, 5, 6, 7]
+        assert axis == [3, 3, 2, 4, 4, -1, -1, -1] and order == [1, 0, 3, 4, 2, 5, 6, 7]
     if name == "tilted":
-        assert axis == [-1, -1, -1, -1, 0, 0, 2, 1, 1] and order == [4, 5, 7, 8, 6, 3, 0, 1, 2]
+        assert axis == [-1, -1, -1, -1, 3, 3, 2, 4, 4] and order == [5, 4, 7, 8, 6, 3, 0, 1, 2]
     if name == "simple":  # no huge sphere: index order
         assert axis == [-1] * 5 and order == list(range(5))
 
