@@ -137,6 +137,34 @@ def test_wall_pairs_with_origins_outside_the_room(cam_pos):
     assert gsegs == rsegs
 
 
+@pytest.mark.parametrize("variant", ["crossed", "double_right", "no_left"])
+def test_wall_pair_degenerate_layouts(variant):
+    """Wall pairs in odd rooms: crossed walls (the - wall's plane beyond the +
+    wall's: every origin counts as outside, both walls tested), a second
+    right wall (unpaired, tested by every ray after the pair), no left wall
+    (no x pair).  Bit-exact with the oracle, and the library's layout equals
+    the oracle's."""
+    _require_gpu()
+    W, H, samps = 48, 32, 8
+    scn = ptgpu.make_scene("box", W, H)
+    R = 1e6
+    if variant == "crossed":
+        scn.spheres[0] = ptgpu.sphere(R, (-R + 0.5, 0.0, -1.0), (0.0, 0.0, 0.0), (0.9, 0.1, 0.2),
+                                      ptgpu.reflection_type.diffuse)
+    elif variant == "double_right":
+        scn.spheres.append(ptgpu.sphere(R, (R + 0.3, 0.0, -1.0), (0.0, 0.0, 0.0), (0.2, 0.8, 0.8),
+                                        ptgpu.reflection_type.specular))
+    else:
+        scn.spheres = scn.spheres[1:]
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    sp, ca = _oracle_scene(scn, cam)
+    assert ptgpu.scene_layout(scn, cam) == po.scan_layout(sp, ca)
+    gpu, gsegs = _gpu_image(scn, cam, W, H, samps, count_segments=True)
+    ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
+    _check_equal(gpu, ref)
+    assert gsegs == rsegs
+
+
 @pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:3000"])
 def test_per_path_radiance_bitexact(name):
     _require_gpu()
