@@ -217,6 +217,35 @@ inline std::vector<BvhNodeHost> order_bvh(const BvhBuild &b, int octant)
     return out;
 }
 
+// Direction-sign bits worth a layout of their own (order_bvh): an axis
+// whose splits carry under 5 % of the tree's weight (each inner node weighs
+// its sphere count, so every level weighs about n) is dropped -- rays that
+// differ only in that sign share a layout, which halves the nodes' cache
+// footprint per dropped axis (10,000-sphere field, thin in y: 1 % faster).
+inline int bvh_octant_mask(const BvhBuild &b)
+{
+    if (b.nodes.empty())
+        return 0;
+    std::vector<double> w(b.nodes.size(), 0.0);
+    double per_axis[3] = {0.0, 0.0, 0.0}, total = 0.0;
+    for (int i = (int)b.nodes.size() - 1; i >= 0; --i) {  // children follow their parent
+        const BvhNodeHost &nd = b.nodes[i];
+        if (nd.leaf >= 0) {
+            w[i] = (double)(nd.leaf >> 24);
+            continue;
+        }
+        const int lo = i + 1, hi = b.nodes[lo].skip;
+        w[i] = w[lo] + w[hi];
+        per_axis[b.axis[i]] += w[i];
+        total += w[i];
+    }
+    int mask = 0;
+    for (int k = 0; k < 3; ++k)
+        if (total > 0.0 && per_axis[k] >= 0.05 * total)
+            mask |= 1 << k;
+    return mask;
+}
+
 inline BvhBuild build_bvh(const ptg_sphere *s, int n, double big_radius)
 {
     BvhBuild b;

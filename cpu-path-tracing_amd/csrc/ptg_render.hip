@@ -154,6 +154,7 @@ struct KArgs {
     // order_bvh), layout k at node index k << bvh_shift, skip words absolute;
     // a walk is done when (ni & bvh_mask) reaches n_nodes
     int bvh_shift, bvh_mask;
+    int bvh_oct_mask;  // direction-sign bits that select the layout (x 1, y 2, z 4): bvh_octant_mask
     const float2 *trig;  // {cos, sin}(2 pi k / 128), staged in LDS (sincos2pi_tab)
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
     float pos_x, pos_y, pos_z;
@@ -415,7 +416,7 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 #if PTG_BVH_OCTANTS
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
-    tr.ni = (int)(oct << A.bvh_shift);
+    tr.ni = (int)((oct & (unsigned)A.bvh_oct_mask) << A.bvh_shift);
 #else
     tr.ni = 0;
 #endif
@@ -1552,6 +1553,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         }
         A.bvh_shift = shift;
         A.bvh_mask = (int)(stride - 1);
+        A.bvh_oct_mask = PTG_BVH_OCTANTS ? bvh_octant_mask(b) : 0;
         for (int c = 0; c < 3; ++c) {
             A.q_lo[c] = grid.lo[c];
             A.q_scale[c] = grid.scale[c];

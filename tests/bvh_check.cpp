@@ -120,7 +120,9 @@ static void check_scene(const std::vector<ptg_sphere> &s)
         else
             CHECK(z.word == nd.skip, "quantised skip %d", i);
     }
-    std::printf("ok %d spheres %d nodes %zu huge, 8 octant layouts\n", n, nn, b.big.size());
+    const int mask = bvh_octant_mask(b);
+    CHECK(nn <= 1 || (mask >= 0 && mask <= 7), "octant mask %d", mask);
+    std::printf("ok %d spheres %d nodes %zu huge, 8 octant layouts, octant mask %d\n", n, nn, b.big.size(), mask);
 }
 
 int main()
