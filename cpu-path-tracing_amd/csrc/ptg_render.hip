@@ -95,6 +95,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_TAIL_CHUNKS
 #define PTG_TAIL_CHUNKS 8  // split-tail units per pixel group of the last rows (1: off)
 #endif
+#ifndef PTG_TAIL_CHUNKS_MANY
+// ... with at least 5 rounds of wave slots (measured: box 1024x768x256 spp
+// 2 % faster with 4 than with 8, the 1920x1080 frame the same; 2-8-way shards
+// of that frame, 2-4 rounds, keep 8)
+#define PTG_TAIL_CHUNKS_MANY 4
+#endif
 #ifndef PTG_TAIL_MIN_HALF_ROUNDS
 // linear scenes: split tail from 1.5 rounds of wave slots on (measured with
 // tools/shard_sim.py: 2/4/8-way shards of the bench frame 1.6/1.8/1.4 %
@@ -1406,7 +1412,8 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
         tail_rows = tail_rows < A.slab_rows ? tail_rows : A.slab_rows;
         A.tail_group = (A.slab_rows - tail_rows) * A.waves_per_row;
         A.n_head_chunks = 1;
-        A.tail_chunk = (nsamp + PTG_TAIL_CHUNKS - 1) / PTG_TAIL_CHUNKS;
+        const int tc = groups >= 5LL * ctx->wave_slots ? PTG_TAIL_CHUNKS_MANY : PTG_TAIL_CHUNKS;
+        A.tail_chunk = (nsamp + tc - 1) / tc;
         const int tail_chunks = (nsamp + A.tail_chunk - 1) / A.tail_chunk;
         A.resolve_row0 = A.slab_rows - tail_rows;
         A.n_units = (long long)A.tail_group + (long long)(groups - A.tail_group) * tail_chunks;
