@@ -66,6 +66,7 @@ int fail(int code, const std::string &msg)
 #define PTG_TRIG_LDS 1  // linear-scene render kernel: sin/cos table in LDS (0: read through L1)
 #endif
 constexpr int kBlock = PTG_BLOCK;
+constexpr int kMaxLevels = 4;     // unit levels: head + up to 3 split-tail levels
 constexpr int kTraceBlock = 256;  // parity probe kernel
 #ifndef PTG_MAX_LDS_SPHERES
 #define PTG_MAX_LDS_SPHERES 64
@@ -94,6 +95,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #endif
 #ifndef PTG_TAIL_CHUNKS
 #define PTG_TAIL_CHUNKS 8  // split-tail units per pixel group of the last rows (1: off)
+#endif
+#ifndef PTG_TAIL_LEVELS
+// split-tail levels, each with twice the chunks of the one before (<= 3);
+// measured: 2 or 3 levels (chunks 4/8/16) within 1 % of 1 level on the bench
+// frame, its 2-8-way shards and box 1024x768
+#define PTG_TAIL_LEVELS 1
 #endif
 #ifndef PTG_TAIL_CHUNKS_MANY
 // ... with at least 5 rounds of wave slots (measured: box 1024x768x256 spp
@@ -174,11 +181,15 @@ struct KArgs {
     float invW, invH, inv_samps, sub_len, inv_sub2;
     unsigned long long seed;
     int chunk, n_groups, single_chunk;
-    // split tail (fill_launch): groups [tail_group, n_groups) -- the last rows
-    // -- run as tail_chunks units of tail_chunk samples each (accumulated,
-    // then resolve_kernel from slab row resolve_row0); tail_group = n_groups
-    // when the whole grid is one kind of unit
-    int tail_group, n_head_chunks, tail_chunk, resolve_row0;
+    // unit levels (fill_launch): level l covers pixel groups [lvl_group[l],
+    // lvl_group[l + 1]) in chunks of lvl_chunk[l] samples, chunk-major, as
+    // units [lvl_unit[l], lvl_unit[l + 1]); level 0 is the head, levels >= 1
+    // the split tail (accumulated, then resolve_kernel from slab row
+    // resolve_row0).  lvl_group[n_levels] = n_groups.
+    int n_levels;
+    int lvl_group[kMaxLevels + 1], lvl_chunk[kMaxLevels];
+    long long lvl_unit[kMaxLevels + 1];
+    int resolve_row0;
     int sample_begin, sample_end;  // samples [begin, end) of every sub-pixel in this launch
     int keep_acc;                  // resolve without re-zeroing (progressive previews)
     int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
@@ -692,25 +703,19 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     const long long unit = (long long)blockIdx.x * kWaves + wv;
     if (unit >= A.n_units)
         return;  // whole wave
-    // head units: groups [0, tail_group) x n_head_chunks chunks of A.chunk
-    // samples, chunk-major (neighbours are different pixel groups); then the
-    // split tail (fill_launch): the last groups in chunks of A.tail_chunk
-    const long long head_units = (long long)A.tail_group * A.n_head_chunks;
-    int group, s0, len;
-    bool in_wave;  // the unit holds every sample of its pixels: resolve in the wave
-    if (unit < head_units) {
-        group = (int)(unit % A.tail_group);
-        s0 = A.sample_begin + (int)(unit / A.tail_group) * A.chunk;
-        len = A.chunk;
-        in_wave = A.single_chunk;
-    } else {
-        const long long t = unit - head_units;
-        const int ntail = A.n_groups - A.tail_group;
-        group = A.tail_group + (int)(t % ntail);
-        s0 = A.sample_begin + (int)(t / ntail) * A.tail_chunk;
-        len = A.tail_chunk;
-        in_wave = false;
-    }
+    // unit -> level (wave-uniform: a few scalar compares) -> pixel group and
+    // sample chunk; chunk-major within a level (neighbours are different
+    // pixel groups)
+    int lv = 0;
+    while (lv + 1 < A.n_levels && unit >= A.lvl_unit[lv + 1])
+        ++lv;
+    const long long t = unit - A.lvl_unit[lv];
+    const int nlg = A.lvl_group[lv + 1] - A.lvl_group[lv];
+    const int group = A.lvl_group[lv] + (int)(t % nlg);
+    const int len = A.lvl_chunk[lv];
+    const int s0 = A.sample_begin + (int)(t / nlg) * len;
+    // the unit holds every sample of its pixels: resolve in the wave
+    const bool in_wave = lv == 0 && A.single_chunk;
     const int slab_row = group / A.waves_per_row;
     const int xblk = group - slab_row * A.waves_per_row;
     const int r = out_row_of(A, slab_row);
@@ -1398,25 +1403,44 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     // in-wave resolve only when one unit holds ALL samples of its pixels
     A.single_chunk = !accumulate_only && n_chunks <= 1 && s_begin == 0 && s_end == p->samples;
     A.n_units = (long long)A.n_groups * n_chunks;
-    A.tail_group = groups;
-    A.n_head_chunks = n_chunks;
-    A.tail_chunk = chunk;
+    A.n_levels = 1;
+    A.lvl_group[0] = 0;
+    A.lvl_group[1] = groups;
+    A.lvl_chunk[0] = chunk;
+    A.lvl_unit[0] = 0;
+    A.lvl_unit[1] = A.n_units;
     A.resolve_row0 = 0;
     // Split tail: with whole-pixel units, the grid ends when its slowest last
     // units end (a unit is ~1/16 of the frame per wave slot here).  The last
     // rows -- about one round of the device's wave slots -- run instead as
-    // PTG_TAIL_CHUNKS shorter units each, accumulated and resolved by
-    // resolve_kernel; everything before keeps the in-wave resolve.
+    // shorter units, accumulated and resolved by resolve_kernel; everything
+    // before keeps the in-wave resolve.  The tail's rows get shorter units
+    // towards the end (PTG_TAIL_LEVELS levels: the first half of the tail
+    // rows in PTG_TAIL_CHUNKS... chunks, see tail_level_chunks), so the last
+    // units to start are the shortest.
     if (tail_ok && A.single_chunk) {
         int tail_rows = (ctx->wave_slots + A.waves_per_row - 1) / A.waves_per_row;
         tail_rows = tail_rows < A.slab_rows ? tail_rows : A.slab_rows;
-        A.tail_group = (A.slab_rows - tail_rows) * A.waves_per_row;
-        A.n_head_chunks = 1;
-        const int tc = groups >= 5LL * ctx->wave_slots ? PTG_TAIL_CHUNKS_MANY : PTG_TAIL_CHUNKS;
-        A.tail_chunk = (nsamp + tc - 1) / tc;
-        const int tail_chunks = (nsamp + A.tail_chunk - 1) / A.tail_chunk;
-        A.resolve_row0 = A.slab_rows - tail_rows;
-        A.n_units = (long long)A.tail_group + (long long)(groups - A.tail_group) * tail_chunks;
+        const bool many = groups >= 5LL * ctx->wave_slots;
+        // level row counts: halves of what is left, the last level takes the rest
+        int rows_left = tail_rows, row = A.slab_rows - tail_rows;
+        A.resolve_row0 = row;
+        A.lvl_group[1] = row * A.waves_per_row;
+        A.lvl_unit[1] = A.lvl_group[1];  // head: one unit per group
+        int l = 1;
+        for (; l <= PTG_TAIL_LEVELS && rows_left > 0; ++l) {
+            const int rows = l == PTG_TAIL_LEVELS ? rows_left : (rows_left + 1) / 2;
+            const int tc = (many ? PTG_TAIL_CHUNKS_MANY : PTG_TAIL_CHUNKS) << (l - 1);
+            const int ch = (nsamp + tc - 1) / tc;
+            const int nch = (nsamp + ch - 1) / ch;
+            row += rows;
+            rows_left -= rows;
+            A.lvl_chunk[l] = ch;
+            A.lvl_group[l + 1] = row * A.waves_per_row;
+            A.lvl_unit[l + 1] = A.lvl_unit[l] + (long long)(A.lvl_group[l + 1] - A.lvl_group[l]) * nch;
+        }
+        A.n_levels = l;
+        A.n_units = A.lvl_unit[l];
     }
     const int waves_per_block = (ctx->n > kLinearMax ? PTG_BVH_BLOCK : kBlock) / 64;
     grid = (int)((A.n_units + waves_per_block - 1) / waves_per_block);
@@ -1719,7 +1743,7 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     int grid = 0;
     fill_launch(ctx, params, A, grid);
     // several units per pixel, a split tail, or no samples at all
-    const bool resolve = !A.single_chunk || A.tail_group < A.n_groups || grid == 0;
+    const bool resolve = !A.single_chunk || A.n_levels > 1 || grid == 0;
     if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
         return rc;
     A.out = d_slab;
