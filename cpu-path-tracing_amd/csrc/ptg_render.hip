@@ -120,6 +120,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_TAIL_MIN_HALF_ROUNDS
 #define PTG_BVH_TAIL_MIN_HALF_ROUNDS 6  // BVH scenes: split tail from 3 rounds of wave slots on
 #endif
+#ifndef PTG_BOX_MODE
+#define PTG_BOX_MODE 1  // linear scenes: nearest-plane wall first (box mode, scene_scan)
+#endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
                           // (measured with octant layouts + SAH: 6 beats 4 by 7 %, 5 and 7 by 1-2 %)
@@ -154,6 +157,14 @@ struct KArgs {
     // its direction moves toward (d_k >= 0: the + wall)
     int pairs[3];
     float pair_lo[3], pair_hi[3];
+    // box mode (scan_order_of: every axis-anchored wall belongs to the one
+    // pair or is the one single wall of its axis, at least one pair, no
+    // other huge sphere): per axis the + and - walls' records (-1: none) and
+    // tangent planes (+-kFarPlane: none); pair_lo/hi bound the room on every
+    // axis (+-kFarPlane where open)
+    int box_mode;
+    int rec_plus[3], rec_minus[3];  // byte offsets of the records
+    float plane_plus[3], plane_minus[3];
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
     const uint4 *bvh_qnodes;  // the same nodes, compact (bvh_build.hpp BvhNodeQ; render kernel)
@@ -248,8 +259,10 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
 // DESIGN.md "scene scan") are exact early-outs that never let a wave skip the
 // sqrt in practice, so they are left out here (-15 % frame time, same bits).
 constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
+constexpr float kFarPlane = 1e30f;             // box mode: the plane of a missing wall
+constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall skip test
 
-enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4 };
+enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5 };
 
 __device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
@@ -261,9 +274,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     const LinRec *best = recs + A.n;
-    auto test = [&](const int i, auto kind_tag) {
+    auto test_rec = [&](const LinRec *r, auto kind_tag, const int kdyn = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
-        const LinRec *r = recs + i;  // wave-uniform, except for a pair's walls
+        // r is wave-uniform, except for a pair's walls / box mode
         float4 g0 = r->g.g0;
         float4 g1 = r->g.g1;
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
@@ -273,6 +286,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         if constexpr (kKind <= kAxZ) {  // huge sphere anchored on axis k: g0.w = +-R, g1.w = +-2R
             hb = __builtin_fmaf(g0.w, comp(d, kKind), ed);
             c = __builtin_fmaf(g1.w, comp(e, kKind), ee);
+        } else if constexpr (kKind == kAxAny) {  // the same, axis kdyn chosen per lane
+            hb = __builtin_fmaf(g0.w, comp(d, kdyn), ed);
+            c = __builtin_fmaf(g1.w, comp(e, kdyn), ee);
         } else if constexpr (kKind == kBig) {  // general anchored form
             hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
@@ -296,6 +312,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         bq = win ? den : bq;
         best = win ? r : best;
     };
+    auto test = [&](const int i, auto kind_tag) { test_rec(recs + i, kind_tag); };
     // scan order: axis-anchored walls (x, y, z), general huge spheres, small
     // spheres (host: prepare_scan_order)
     int i = 0;
@@ -319,9 +336,70 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         for (; i < A.end_ax[k]; ++i)
             test(i, kind_tag);
     };
-    axis_group(std::integral_constant<int, kAxX>{});
-    axis_group(std::integral_constant<int, kAxY>{});
-    axis_group(std::integral_constant<int, kAxZ>{});
+    if (A.box_mode) {
+        // Box mode (DESIGN.md "box mode"): per axis the wall the ray moves
+        // toward and the distance u/v to its tangent plane; the wall of the
+        // nearest plane is tested first.  Every wall lies beyond its tangent
+        // plane, so another wall can only win if its plane is nearer than the
+        // winner's root (checked with a 2^-12 margin, far above the roots'
+        // rounding): those walls are tested only where that check fails
+        // (rare: rays hitting near an edge), and origins outside the room
+        // test every wall.
+        const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
+                             (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
+        float u[3], v[3];
+        int ci[3];  // record byte offsets, -1: no wall on that side
+        for (int k = 0; k < 3; ++k) {
+            // the uniform plane / record values stay in SGPRs: select values,
+            // not kernel-argument addresses (that became per-lane loads)
+            float pp = A.plane_plus[k], pm = A.plane_minus[k];
+            int rp = A.rec_plus[k], rm = A.rec_minus[k];
+            asm volatile("" : "+s"(pp), "+s"(pm), "+s"(rp), "+s"(rm));
+            const float dk = comp(d, k);
+            const bool pos = dk >= 0.0f;
+            const float diff = (pos ? pp : pm) - comp(o, k);
+            u[k] = pos ? diff : -diff;
+            v[k] = __builtin_fabsf(dk);
+            ci[k] = pos ? rp : rm;
+        }
+        float un = u[0], vn = v[0];
+        int in = ci[0], kn = 0;
+        for (int k = 1; k < 3; ++k) {
+            const bool nearer = u[k] * vn < un * v[k];
+            un = nearer ? u[k] : un;
+            vn = nearer ? v[k] : vn;
+            in = nearer ? ci[k] : in;
+            kn = nearer ? k : kn;
+        }
+        auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
+        test_rec(rec_at(in), std::integral_constant<int, kAxAny>{}, kn);  // in >= 0: some axis has a pair
+        const float bqm = bq * kPlaneMargin;
+        bool need[3];
+        for (int k = 0; k < 3; ++k)
+            need[k] = (ci[k] >= 0) & (k != kn) & !(bn * v[k] < u[k] * bqm);
+        if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
+            if (!in_room) {
+                for (; i < A.end_ax[0]; ++i)
+                    test(i, std::integral_constant<int, kAxX>{});
+                for (; i < A.end_ax[1]; ++i)
+                    test(i, std::integral_constant<int, kAxY>{});
+                for (; i < A.end_ax[2]; ++i)
+                    test(i, std::integral_constant<int, kAxZ>{});
+            } else {
+                if (need[0])
+                    test_rec(rec_at(ci[0]), std::integral_constant<int, kAxX>{});
+                if (need[1])
+                    test_rec(rec_at(ci[1]), std::integral_constant<int, kAxY>{});
+                if (need[2])
+                    test_rec(rec_at(ci[2]), std::integral_constant<int, kAxZ>{});
+            }
+        }
+        i = A.end_ax[2];
+    } else {
+        axis_group(std::integral_constant<int, kAxX>{});
+        axis_group(std::integral_constant<int, kAxY>{});
+        axis_group(std::integral_constant<int, kAxZ>{});
+    }
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
     for (; i < A.n; ++i)
@@ -1269,6 +1347,62 @@ void pair_walls(const ptg_sphere *s, int n, const std::vector<int> &axis, const 
     }
 }
 
+// Box mode (scene_scan; DESIGN.md "box mode"): on when every axis-anchored
+// wall is either one of its axis's pair or the only wall of its axis, at
+// least one axis has a pair, and there is no other huge sphere.  Fills the
+// per-axis records (scan positions in `order`) and tangent planes (the
+// records' anchor coordinate), and extends the pair bounds to single walls
+// (margin as pair_walls) and open sides (+-kFarPlane).  The oracle's prep_B
+// makes the same choice.
+void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
+                 const std::vector<GeoRec> &geo, const std::vector<int> &order, KArgs &A)
+{
+    A.box_mode = 0;
+    int cnt[3] = {0, 0, 0}, general = 0;
+    for (int i = 0; i < n; ++i) {
+        if (s[i].radius < kBigRadius)
+            continue;
+        if (axis[i] < 0)
+            ++general;
+        else
+            ++cnt[axis[i]];
+    }
+    bool ok = general == 0 && (A.pairs[0] || A.pairs[1] || A.pairs[2]);
+    for (int k = 0; k < 3; ++k)
+        ok = ok && (A.pairs[k] ? cnt[k] == 2 : cnt[k] <= 1);
+    if (!ok)
+        return;
+    const SceneBox box = scene_box(s, n, cam);
+    const double margin = 1e-4 * std::max(1.0, box.diag);
+    for (int k = 0; k < 3; ++k) {
+        A.rec_plus[k] = A.rec_minus[k] = -1;
+        A.plane_plus[k] = kFarPlane;
+        A.plane_minus[k] = -kFarPlane;
+        const int begin = k == 0 ? 0 : A.end_ax[k - 1];
+        for (int j = begin; j < A.end_ax[k]; ++j) {
+            const int i = order[j];
+            const float nk = (&geo[i].g1.x)[k];  // anchor normal component: exactly +-1
+            const float plane = (&geo[i].g0.x)[k];  // the anchor point's coordinate
+            if (nk < 0.0f) {  // centre on the + side
+                A.rec_plus[k] = j * (int)sizeof(LinRec);
+                A.plane_plus[k] = plane;
+                if (!A.pairs[k])
+                    A.pair_hi[k] = (float)(s[i].position[k] - s[i].radius + margin);
+            } else {
+                A.rec_minus[k] = j * (int)sizeof(LinRec);
+                A.plane_minus[k] = plane;
+                if (!A.pairs[k])
+                    A.pair_lo[k] = (float)(s[i].position[k] + s[i].radius - margin);
+            }
+        }
+        if (A.rec_plus[k] < 0)
+            A.pair_hi[k] = kFarPlane;
+        if (A.rec_minus[k] < 0)
+            A.pair_lo[k] = -kFarPlane;
+    }
+    A.box_mode = 1;
+}
+
 // Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z
 // (each axis group led by its wall pair, + wall first), then the other huge
 // spheres, then the small ones, each group otherwise in scene index order;
@@ -1290,6 +1424,7 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam
                 order.push_back(i);
         A.end_ax[k] = (int)order.size();
     }
+    box_mode_of(s, n, cam, axis, geo, order, A);
     for (int i = 0; i < n; ++i)
         if (s[i].radius >= kBigRadius && axis[i] < 0)
             order.push_back(i);
@@ -1552,7 +1687,12 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         A.pairs[k] = order.pairs[k];
         A.pair_lo[k] = order.pair_lo[k];
         A.pair_hi[k] = order.pair_hi[k];
+        A.rec_plus[k] = order.rec_plus[k];
+        A.rec_minus[k] = order.rec_minus[k];
+        A.plane_plus[k] = order.plane_plus[k];
+        A.plane_minus[k] = order.plane_minus[k];
     }
+    A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
     A.end_big = order.end_big;
     if ((int)n_spheres > kLinearMax) {
         BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);

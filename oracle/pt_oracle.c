@@ -607,7 +607,8 @@ typedef struct {
     int axis;         /* huge sphere anchored on axis 0..2, else -1 (choose_anchor_B) */
     int visit;        /* linear scan: the sphere visited at scan position (this element's index) */
     int pair;         /* wall pair member (pair_walls_B): +1 the + wall, -1 the - wall, 0 none */
-    float plo, phi;   /* on the + wall: the pair's origin bounds */
+    float plo, phi;   /* on the + wall: the pair's origin bounds; box mode: a single wall's bound */
+    int box;          /* box mode (box_mode_B), the same on every element */
 } sphB;
 
 typedef struct {
@@ -708,6 +709,44 @@ static void pair_walls_B(const po_sphere *s, int n, const boxB *box, sphB *out)
     }
 }
 
+/* Box mode (DESIGN.md "box mode"; the kernel's host side: ptg_render.hip
+ * box_mode_of): every axis-anchored wall is one of its axis's pair or the
+ * only wall of its axis, some axis has a pair, no other huge sphere.  A
+ * single wall's room bound (margin as pair_walls_B) goes into its own
+ * plo (- side wall) or phi (+ side wall). */
+static void box_mode_B(const po_sphere *s, int n, const boxB *box, sphB *out)
+{
+    int cnt[3] = {0, 0, 0}, pairs[3] = {0, 0, 0}, general = 0;
+    for (int i = 0; i < n; ++i) {
+        out[i].box = 0;
+        if (!out[i].big)
+            continue;
+        if (out[i].axis < 0)
+            ++general;
+        else
+            ++cnt[out[i].axis];
+        if (out[i].pair == 1)
+            pairs[out[i].axis] = 1;
+    }
+    int ok = general == 0 && (pairs[0] || pairs[1] || pairs[2]);
+    for (int k = 0; k < 3; ++k)
+        ok = ok && (pairs[k] ? cnt[k] == 2 : cnt[k] <= 1);
+    if (!ok)
+        return;
+    const double margin = 1e-4 * (box->diag > 1.0 ? box->diag : 1.0);
+    for (int i = 0; i < n; ++i) {
+        out[i].box = 1;
+        if (out[i].big && out[i].pair == 0) { /* single wall */
+            const int k = out[i].axis;
+            const float nk = k == 0 ? out[i].N.x : (k == 1 ? out[i].N.y : out[i].N.z);
+            if (nk < 0.0f)
+                out[i].phi = (float)(s[i].position[k] - s[i].radius + margin);
+            else
+                out[i].plo = (float)(s[i].position[k] + s[i].radius - margin);
+        }
+    }
+}
+
 static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
 {
     boxB box = scene_box_B(s, n, cam);
@@ -723,6 +762,7 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         b->axis = -1;
         b->pair = 0;
         b->plo = b->phi = 0.0f;
+        b->box = 0;
         if (b->big) {
             double P[3], N[3];
             b->axis = choose_anchor_B(sp, cam, &box, P, N);
@@ -753,6 +793,7 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
      * ones; each group otherwise in index order */
     if (n <= LINEAR_MAX_PREP) {
         pair_walls_B(s, n, &box, out);
+        box_mode_B(s, n, &box, out);
         int j = 0;
         for (int k = 0; k < 3; ++k) {
             for (int i = 0; i < n; ++i)
@@ -887,6 +928,77 @@ static void test_B(const sphB *sp, int i, f3 o, f3 d, float a, float *bn, float 
     }
 }
 
+#define FAR_PLANE 1e30f
+#define PLANE_MARGIN 0x1.ffep-1f /* 1 - 2^-12 */
+static float fcomp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+/* Box mode walls (the kernel's scene_scan): the wall of the nearest tangent
+ * plane the ray moves toward first; another wall only where its plane is not
+ * safely beyond that root, or every wall for an origin outside the room.
+ * Returns the number of scan positions consumed (the walls). */
+static int box_walls_B(const sphB *s, int n, f3 o, f3 d, float a, float *bn, float *bq, int *id)
+{
+    int rec_plus[3] = {-1, -1, -1}, rec_minus[3] = {-1, -1, -1};
+    float plane_plus[3] = {FAR_PLANE, FAR_PLANE, FAR_PLANE}, plane_minus[3] = {-FAR_PLANE, -FAR_PLANE, -FAR_PLANE};
+    float lo[3] = {-FAR_PLANE, -FAR_PLANE, -FAR_PLANE}, hi[3] = {FAR_PLANE, FAR_PLANE, FAR_PLANE};
+    int nw = 0;
+    while (nw < n && s[s[nw].visit].big && s[s[nw].visit].axis >= 0) { /* the walls lead the scan order */
+        const int i = s[nw].visit, k = s[i].axis;
+        const float nk = fcomp(s[i].N, k);
+        if (nk < 0.0f) {
+            rec_plus[k] = i;
+            plane_plus[k] = fcomp(s[i].P, k);
+            if (s[i].pair == 1) {
+                lo[k] = s[i].plo;
+                hi[k] = s[i].phi;
+            } else {
+                hi[k] = s[i].phi;
+            }
+        } else {
+            rec_minus[k] = i;
+            plane_minus[k] = fcomp(s[i].P, k);
+            if (s[i].pair == 0)
+                lo[k] = s[i].plo;
+        }
+        ++nw;
+    }
+    const int in_room = o.x >= lo[0] && o.x <= hi[0] && o.y >= lo[1] && o.y <= hi[1] && o.z >= lo[2] &&
+                        o.z <= hi[2];
+    float u[3], v[3];
+    int ci[3];
+    for (int k = 0; k < 3; ++k) {
+        const float dk = fcomp(d, k);
+        const int pos = dk >= 0.0f;
+        const float diff = (pos ? plane_plus[k] : plane_minus[k]) - fcomp(o, k);
+        u[k] = pos ? diff : -diff;
+        v[k] = fabsf(dk);
+        ci[k] = pos ? rec_plus[k] : rec_minus[k];
+    }
+    float un = u[0], vn = v[0];
+    int in = ci[0], kn = 0;
+    for (int k = 1; k < 3; ++k)
+        if (u[k] * vn < un * v[k]) {
+            un = u[k];
+            vn = v[k];
+            in = ci[k];
+            kn = k;
+        }
+    test_B(&s[in], in, o, d, a, bn, bq, id);
+    const float bqm = *bq * PLANE_MARGIN;
+    int need[3];
+    for (int k = 0; k < 3; ++k)
+        need[k] = ci[k] >= 0 && k != kn && !(*bn * v[k] < u[k] * bqm);
+    if (!in_room) {
+        for (int j = 0; j < nw; ++j)
+            test_B(&s[s[j].visit], s[j].visit, o, d, a, bn, bq, id);
+    } else {
+        for (int k = 0; k < 3; ++k)
+            if (need[k])
+                test_B(&s[ci[k]], ci[k], o, d, a, bn, bq, id);
+    }
+    return nw;
+}
+
 static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
 {
     /* nearest root kept as a fraction bn/bq (bq > 0): candidates are compared
@@ -894,7 +1006,10 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
     float a = fdot(d, d);
     float bn = INFF, bq = 1.0f;
     int id = -1;
-    for (int j = 0; j < n; ++j) {
+    int j0 = 0;
+    if (n > 0 && s[0].box)
+        j0 = box_walls_B(s, n, o, d, a, &bn, &bq, &id);
+    for (int j = j0; j < n; ++j) {
         const int i = s[j].visit; /* scan order: first visited wins exact ties */
         if (s[i].pair == 1) { /* wall pair: + wall at j, - wall at j + 1 */
             const int im = s[j + 1].visit, k = s[i].axis;
