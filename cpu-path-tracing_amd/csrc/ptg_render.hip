@@ -357,8 +357,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             asm volatile("" : "+s"(pp), "+s"(pm), "+s"(rp), "+s"(rm));
             const float dk = comp(d, k);
             const bool pos = dk >= 0.0f;
-            const float diff = (pos ? pp : pm) - comp(o, k);
-            u[k] = pos ? diff : -diff;
+            // (o - pm) is the same IEEE subtraction as -(pm - o).  A missing
+            // wall's plane is at +-kFarPlane: u ~ 1e30 is never the nearest
+            // and never needed below
+            const float up = pp - comp(o, k), um = comp(o, k) - pm;
+            u[k] = pos ? up : um;
             v[k] = __builtin_fabsf(dk);
             ci[k] = pos ? rp : rm;
         }
@@ -376,7 +379,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         const float bqm = bq * kPlaneMargin;
         bool need[3];
         for (int k = 0; k < 3; ++k)
-            need[k] = (ci[k] >= 0) & (k != kn) & !(bn * v[k] < u[k] * bqm);
+            need[k] = (k != kn) & !(bn * v[k] < u[k] * bqm);
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             if (!in_room) {
                 for (; i < A.end_ax[0]; ++i)

@@ -969,8 +969,7 @@ static int box_walls_B(const sphB *s, int n, f3 o, f3 d, float a, float *bn, flo
     for (int k = 0; k < 3; ++k) {
         const float dk = fcomp(d, k);
         const int pos = dk >= 0.0f;
-        const float diff = (pos ? plane_plus[k] : plane_minus[k]) - fcomp(o, k);
-        u[k] = pos ? diff : -diff;
+        u[k] = pos ? plane_plus[k] - fcomp(o, k) : fcomp(o, k) - plane_minus[k];
         v[k] = fabsf(dk);
         ci[k] = pos ? rec_plus[k] : rec_minus[k];
     }
@@ -987,7 +986,7 @@ static int box_walls_B(const sphB *s, int n, f3 o, f3 d, float a, float *bn, flo
     const float bqm = *bq * PLANE_MARGIN;
     int need[3];
     for (int k = 0; k < 3; ++k)
-        need[k] = ci[k] >= 0 && k != kn && !(*bn * v[k] < u[k] * bqm);
+        need[k] = k != kn && !(*bn * v[k] < u[k] * bqm); /* a missing wall: u ~ 1e30, never needed */
     if (!in_room) {
         for (int j = 0; j < nw; ++j)
             test_B(&s[s[j].visit], s[j].visit, o, d, a, bn, bq, id);
