@@ -274,7 +274,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     const LinRec *best = recs + A.n;
-    auto test_rec = [&](const LinRec *r, auto kind_tag, const int kdyn = 0) {
+    auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f) {
         constexpr int kKind = decltype(kind_tag)::value;
         // r is wave-uniform, except for a pair's walls / box mode
         float4 g0 = r->g.g0;
@@ -286,9 +286,13 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         if constexpr (kKind <= kAxZ) {  // huge sphere anchored on axis k: g0.w = +-R, g1.w = +-2R
             hb = __builtin_fmaf(g0.w, comp(d, kKind), ed);
             c = __builtin_fmaf(g1.w, comp(e, kKind), ee);
-        } else if constexpr (kKind == kAxAny) {  // the same, axis kdyn chosen per lane
-            hb = __builtin_fmaf(g0.w, comp(d, kdyn), ed);
-            c = __builtin_fmaf(g1.w, comp(e, kdyn), ee);
+        } else if constexpr (kKind == kAxAny) {
+            // the same, for the wall the ray moves toward on a per-lane axis
+            // k: g0.w d_k = -R |d_k| = -|g0.w| vn and g1.w e_k = 2R u = |g1.w| un
+            // (un: the plane distance numerator, the same subtraction as e_k
+            // up to sign), the products' bits are unchanged
+            hb = __builtin_fmaf(-__builtin_fabsf(g0.w), vn, ed);
+            c = __builtin_fmaf(__builtin_fabsf(g1.w), un, ee);
         } else if constexpr (kKind == kBig) {  // general anchored form
             hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
@@ -375,7 +379,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             kn = nearer ? k : kn;
         }
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
-        test_rec(rec_at(in), std::integral_constant<int, kAxAny>{}, kn);  // in >= 0: some axis has a pair
+        test_rec(rec_at(in), std::integral_constant<int, kAxAny>{}, un, vn);  // in >= 0: some axis has a pair
         const float bqm = bq * kPlaneMargin;
         bool need[3];
         for (int k = 0; k < 3; ++k)
