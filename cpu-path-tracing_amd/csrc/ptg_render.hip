@@ -351,14 +351,15 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // test every wall.
         const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
                              (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
+        // wall table after the sentinel: byte offsets of the records of axis
+        // k's + wall (2k) and - wall (2k + 1), -1 where missing
+        const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
         float u[3], v[3];
-        int ci[3];  // record byte offsets, -1: no wall on that side
         for (int k = 0; k < 3; ++k) {
             // the uniform plane / record values stay in SGPRs: select values,
             // not kernel-argument addresses (that became per-lane loads)
             float pp = A.plane_plus[k], pm = A.plane_minus[k];
-            int rp = A.rec_plus[k], rm = A.rec_minus[k];
-            asm volatile("" : "+s"(pp), "+s"(pm), "+s"(rp), "+s"(rm));
+            asm volatile("" : "+s"(pp), "+s"(pm));
             const float dk = comp(d, k);
             const bool pos = dk >= 0.0f;
             // (o - pm) is the same IEEE subtraction as -(pm - o).  A missing
@@ -367,17 +368,16 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             const float up = pp - comp(o, k), um = comp(o, k) - pm;
             u[k] = pos ? up : um;
             v[k] = __builtin_fabsf(dk);
-            ci[k] = pos ? rp : rm;
         }
         float un = u[0], vn = v[0];
-        int in = ci[0], kn = 0;
+        int kn = 0;
         for (int k = 1; k < 3; ++k) {
             const bool nearer = u[k] * vn < un * v[k];
             un = nearer ? u[k] : un;
             vn = nearer ? v[k] : vn;
-            in = nearer ? ci[k] : in;
             kn = nearer ? k : kn;
         }
+        const int in = walls[2 * kn + (comp(d, kn) >= 0.0f ? 0 : 1)];
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         test_rec(rec_at(in), std::integral_constant<int, kAxAny>{}, un, vn);  // in >= 0: some axis has a pair
         const float bqm = bq * kPlaneMargin;
@@ -393,12 +393,13 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 for (; i < A.end_ax[2]; ++i)
                     test(i, std::integral_constant<int, kAxZ>{});
             } else {
+                auto wall = [&](int k) { return rec_at(walls[2 * k + (comp(d, k) >= 0.0f ? 0 : 1)]); };
                 if (need[0])
-                    test_rec(rec_at(ci[0]), std::integral_constant<int, kAxX>{});
+                    test_rec(wall(0), std::integral_constant<int, kAxX>{});
                 if (need[1])
-                    test_rec(rec_at(ci[1]), std::integral_constant<int, kAxY>{});
+                    test_rec(wall(1), std::integral_constant<int, kAxY>{});
                 if (need[2])
-                    test_rec(rec_at(ci[2]), std::integral_constant<int, kAxZ>{});
+                    test_rec(wall(2), std::integral_constant<int, kAxZ>{});
             }
         }
         i = A.end_ax[2];
@@ -776,7 +777,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             lds_trig[i] = A.trig[i];
         trig = lds_trig;
 #endif
-        for (int i = threadIdx.x; i <= A.n; i += kBlock)  // n records + the sentinel
+        for (int i = threadIdx.x; i <= A.n + 1; i += kBlock)  // n records + the sentinel + the wall table
             lds_lin[i] = A.lin[i];
         recs = lds_lin;
     }
@@ -1652,10 +1653,16 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     std::vector<LinRec> lin;
     if (linear) {  // the scan's record order, interleaved, + the no-hit sentinel
         prepare_scan_order(spheres, (int)n_spheres, cam, geo, shade, axis, lgeo, lshade, order);
-        lin.resize(n_spheres + 1);
+        lin.resize(n_spheres + 2);  // + the box-mode wall table (scene_scan)
         std::memset(lin.data(), 0, lin.size() * sizeof(LinRec));
         for (size_t i = 0; i < n_spheres; ++i)
             lin[i] = LinRec{lgeo[i], lshade[i]};
+        int32_t walls[6];
+        for (int k = 0; k < 3; ++k) {
+            walls[2 * k] = order.rec_plus[k];
+            walls[2 * k + 1] = order.rec_minus[k];
+        }
+        std::memcpy(&lin[n_spheres + 1], walls, sizeof(walls));
     }
     ptg_context *ctx = new ptg_context();
     ctx->device = dev;
@@ -1852,7 +1859,7 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     if (grid <= 0)
         return PTG_OK;
     const bool bvh = A.n > kLinearMax;
-    const size_t lds = bvh ? 0 : (size_t)(A.n + 1) * sizeof(LinRec);
+    const size_t lds = bvh ? 0 : (size_t)(A.n + 2) * sizeof(LinRec);
     if (count)
         bvh ? render_kernel<true, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A)
             : render_kernel<true, false><<<grid, kBlock, lds, s>>>(A);
