@@ -215,17 +215,31 @@ struct Lane {
     uint64_t key;
 };
 
-__device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32_t sample, uint32_t &st, f3 &o,
+// camera constants as 4 float4: {pos, lens}, {base, sub_len}, {X, 1/W},
+// {Y, 1/H}.  The render kernel stages them in LDS and reads them in each
+// refill (camera_ray runs only there): kept in registers for the whole unit
+// they took 16 VGPRs, half of them spilled to scratch (measured).
+struct CamC {
+    float4 p, b, X, Y;
+};
+
+__host__ __device__ inline CamC cam_of(const KArgs &A)
+{
+    return CamC{make_float4(A.pos_x, A.pos_y, A.pos_z, A.lens), make_float4(A.base_x, A.base_y, A.base_z, A.sub_len),
+                make_float4(A.X_x, A.X_y, A.X_z, A.invW), make_float4(A.Y_x, A.Y_y, A.Y_z, A.invH)};
+}
+
+__device__ __forceinline__ void camera_ray(const CamC &C, const Lane &L, uint32_t sample, uint32_t &st, f3 &o,
                                            f3 &d)
 {
     st = sample_state(L.key, sample);
     // main.cpp:186-190: jitter inside the sub-pixel cell
     float u1 = draw(st);
     float u2 = draw(st);
-    float xin = __builtin_fmaf(A.sub_len, u1, (float)L.x + (float)L.sx * A.sub_len);
-    float yin = __builtin_fmaf(A.sub_len, u2, (float)L.y + (float)L.sy * A.sub_len);
-    float fs = xin * A.invW;  // main.cpp:190 x/W as x * (1/W)
-    float ft = yin * A.invH;
+    float xin = __builtin_fmaf(C.b.w, u1, (float)L.x + (float)L.sx * C.b.w);
+    float yin = __builtin_fmaf(C.b.w, u2, (float)L.y + (float)L.sy * C.b.w);
+    float fs = xin * C.X.w;  // main.cpp:190 x/W as x * (1/W)
+    float ft = yin * C.Y.w;
     // camera.cpp:19-30: rejection sample of the unit disk (2 draws per try)
     float px, py;
     do {
@@ -234,12 +248,12 @@ __device__ __forceinline__ void camera_ray(const KArgs &A, const Lane &L, uint32
     } while (__builtin_fmaf(py, py, px * px) >= 1.0f);
     // camera.cpp:34-37 (offset = rd*s + rd*t, the reference's lens quirk)
     float sst = fs + ft;
-    float ox = (px * A.lens) * sst;
-    float oy = (py * A.lens) * sst;
-    o = mk3(A.pos_x + ox, A.pos_y + oy, A.pos_z);
-    d = mk3(__builtin_fmaf(A.Y_x, ft, __builtin_fmaf(A.X_x, fs, A.base_x)) - ox,
-            __builtin_fmaf(A.Y_y, ft, __builtin_fmaf(A.X_y, fs, A.base_y)) - oy,
-            __builtin_fmaf(A.Y_z, ft, __builtin_fmaf(A.X_z, fs, A.base_z)));
+    float ox = (px * C.p.w) * sst;
+    float oy = (py * C.p.w) * sst;
+    o = mk3(C.p.x + ox, C.p.y + oy, C.p.z);
+    d = mk3(__builtin_fmaf(C.Y.x, ft, __builtin_fmaf(C.X.x, fs, C.b.x)) - ox,
+            __builtin_fmaf(C.Y.y, ft, __builtin_fmaf(C.X.y, fs, C.b.y)) - oy,
+            __builtin_fmaf(C.Y.z, ft, __builtin_fmaf(C.X.z, fs, C.b.z)));
 }
 
 // main.cpp:30-42 + sphere.cpp:6-30: closest root >= eps over all spheres,
@@ -781,6 +795,14 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             lds_lin[i] = A.lin[i];
         recs = lds_lin;
     }
+    __shared__ float4 lds_cam[4];
+    if (threadIdx.x == 0) {
+        const CamC c = cam_of(A);
+        lds_cam[0] = c.p;
+        lds_cam[1] = c.b;
+        lds_cam[2] = c.X;
+        lds_cam[3] = c.Y;
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the compiler keep all
@@ -857,7 +879,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         L.sx = (int)((pk >> 20) & 63u);
         L.sy = (int)(pk >> 26);
         L.key = lds_key[wv][sl];
-        camera_ray(A, L, (uint32_t)sample, rs, ro, rd);
+        // the index is opaque to the compiler, so the reads stay here
+        // instead of being hoisted into registers live for the whole unit
+        int ci = 0;
+        asm volatile("" : "+v"(ci));
+        const CamC C{lds_cam[ci], lds_cam[ci + 1], lds_cam[ci + 2], lds_cam[ci + 3]};
+        camera_ray(C, L, (uint32_t)sample, rs, ro, rd);
     };
     int phase = 0;  // BVH scenes: 0 fresh ray, 1 walking, 2 scan done (resumable scan, see below)
     auto begin = [&](int it, f3 ro, f3 rd, uint32_t rs) {
@@ -1137,7 +1164,7 @@ __global__ __launch_bounds__(kTraceBlock) void trace_kernel(KArgs A, const int32
     L.key = key_hash(A.seed, pixel_sub);
     f3 o, d;
     uint32_t st;
-    camera_ray(A, L, sample, st, o, d);
+    camera_ray(cam_of(A), L, sample, st, o, d);
     f3 T = mk3(1.0f, 1.0f, 1.0f), E = mk3(0.0f, 0.0f, 0.0f);
     int depth = 0, segs = 0;
     bool done = false;
