@@ -264,6 +264,10 @@ def main():
                          "traffic": traffic,
                          "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
                          "segments_per_sample": round(s_bar, 4),
+                         # SURVEY.md 8(d)'s conservative "tests-only" model: S_bar*N*23
+                         # (linear scenes; the BVH kernel's executed sphere tests otherwise)
+                         "frac_tests_only": round(my_samples * 23 * tests_per_sample / (kern_ms / 1e3) / 1e12
+                                                  / PEAK_FP32_TFLOPS, 4) if kern_ms > 0 else None,
                          "sphere_tests_per_segment": round(tests_per_sample / s_bar, 2) if s_bar else None,
                          "box_tests_per_segment": round(boxes_per_sample / s_bar, 2) if s_bar else None,
                          "scan": "bvh" if n_sph > 64 else "linear",
