@@ -85,7 +85,7 @@ constexpr int kMaxLdsSpheres = PTG_MAX_LDS_SPHERES;
 constexpr int kLinearMax = PTG_LINEAR_MAX;
 static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_REFILL_BATCH
-#define PTG_REFILL_BATCH 32  // measured: 32 beats 16 and ties 48 (DESIGN.md perf log)
+#define PTG_REFILL_BATCH 40  // measured: 40 beats 32 by 0.35 % (box) / 0.6 % (box_mirror), ties 48-56; 24 is 1.2 % slower
 #endif
 #ifndef PTG_LEAF_FRAC
 #define PTG_LEAF_FRAC 6  // BVH: leaf phase once 6/8 of the walking lanes hold a leaf (measured: 6 beats 4 by 2 %)
