@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Whole-frame parity evidence at a BASELINE.json configuration (not a pytest
+case: the CPU side takes a minute or more).
+
+Renders one full frame on cuda:0 through the C ABI and the same frame with
+the oracle's Mode B (the fp32 restatement, the bit-exact checker) on the host
+cores, and reports max |diff| and per-pixel RMSE over all pixels and channels
+(SURVEY.md 8(d)).  With --f64 it also renders Mode A/xs (double arithmetic,
+same counter RNG) and reports the RMSE of the GPU frame against it: the
+effect of computing in fp32, against the north star's 1e-3.
+
+Usage (GPU box, repo root):
+  python tools/full_frame_parity.py --scene box --width 1024 --height 768 --spp 256 --f64 \
+      --out gpurun_out/parity_c2.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cpu-path-tracing_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import ptgpu  # noqa: E402
+import pyoracle as po  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="box")
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=768)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--f64", action="store_true")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    W, H, nsub = a.width, a.height, 2
+    samps = a.spp // (nsub * nsub)
+    seed = ptgpu.DEFAULT_SEED
+    scn = ptgpu.make_scene(a.scene, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+
+    rows = ptgpu.shard_rows(H, ptgpu.DEFAULT_BAND_ROWS, 1)
+    out = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda:0")
+    t0 = time.perf_counter()
+    with ptgpu.Context(scn, cam, device=0) as ctx:
+        ctx.render_device(out, ptgpu.make_params(W, H, samps, nsub, seed))
+        torch.cuda.synchronize()
+    t_gpu = time.perf_counter() - t0
+    gpu = out.cpu().numpy().reshape(rows, W, 3)[:H].astype(np.float64)
+    print(f"gpu frame done ({t_gpu:.2f} s incl. setup)", file=sys.stderr, flush=True)
+
+    sp = scn.to_array().view(po.SPHERE_DT)
+    ca = cam.to_array().view(po.CAMERA_DT)
+    t0 = time.perf_counter()
+    b, _ = po.render_xs_f32(sp, ca, W, H, samps, nsub, seed, nthreads=a.threads)
+    t_b = time.perf_counter() - t0
+    b = b.astype(np.float64)
+    print(f"oracle Mode B frame done ({t_b:.1f} s)", file=sys.stderr, flush=True)
+    res = {
+        "workload": f"{a.scene} {W}x{H} {samps * nsub * nsub}spp",
+        "pixels": W * H,
+        "gpu_seconds_incl_setup": round(t_gpu, 3),
+        "oracle_mode_b_seconds": round(t_b, 1),
+        "oracle_threads": a.threads,
+        "max_abs_vs_mode_b": float(np.abs(gpu - b).max()),
+        "rmse_vs_mode_b": float(np.sqrt(((gpu - b) ** 2).mean())),
+        "pixels_differing_from_mode_b": int((np.abs(gpu - b).max(axis=2) > 0).sum()),
+        "image_mean": float(gpu.mean()),
+    }
+    if a.f64:
+        t0 = time.perf_counter()
+        x, _ = po.render_xs_f64(sp, ca, W, H, samps, nsub, seed, nthreads=a.threads)
+        res["oracle_mode_a_xs_seconds"] = round(time.perf_counter() - t0, 1)
+        res["rmse_vs_mode_a_xs_f64"] = float(np.sqrt(((gpu - x) ** 2).mean()))
+        res["max_abs_vs_mode_a_xs_f64"] = float(np.abs(gpu - x).max())
+        res["rmse_tolerance"] = 1e-3
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+    if res["max_abs_vs_mode_b"] != 0.0:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
