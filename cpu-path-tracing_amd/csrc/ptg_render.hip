@@ -120,6 +120,15 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_TAIL_MIN_HALF_ROUNDS
 #define PTG_BVH_TAIL_MIN_HALF_ROUNDS 6  // BVH scenes: split tail from 3 rounds of wave slots on
 #endif
+#ifndef PTG_BVH_HEAD_CHUNK
+#define PTG_BVH_HEAD_CHUNK 128  // BVH scenes below the split-tail threshold: head rows in chunks of this many samples (0: off; C5 8-way shard 50.4 -> 48.1 ms; 64/96 within 0.5 %, whole pixels +45 %)
+#endif
+#ifndef PTG_BVH_HEAD_TAIL_HALF_ROUNDS
+#define PTG_BVH_HEAD_TAIL_HALF_ROUNDS 1  // ... and the last rows, this many half rounds of wave slots, in the auto chunk (1 beats 2 by 2.5 %, 3 by 5 %)
+#endif
+#ifndef PTG_BVH_TAIL_CHUNK
+#define PTG_BVH_TAIL_CHUNK 0  // ... in chunks of this many samples (0: the auto chunk, 20 at C5 8-way; 10: +0.8 %, 32: +5 %)
+#endif
 #ifndef PTG_SMALL_DISC_SKIP
 #define PTG_SMALL_DISC_SKIP 1  // linear scan: skip a small sphere's root when no lane's disc >= 0 (box -0.9 %, box_mirror -2.1 %, simple -7 %; also skipping spheres behind every lane: +0.1-0.5 %)
 #endif
@@ -1623,6 +1632,33 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
         A.n_levels = l;
         A.n_units = A.lvl_unit[l];
     }
+#if PTG_BVH_HEAD_CHUNK > 0
+    // BVH frames/shards below their split-tail threshold (e.g. 8-way shards
+    // of C5): the head rows run in longer sample chunks -- fewer per-unit
+    // pool tails -- and about the last round of wave slots' rows in the auto
+    // chunk, so the grid still ends on short units.  Every unit accumulates;
+    // resolve_kernel finishes all rows.
+    else if (ctx->n > kLinearMax && p->chunk_samples <= 0 && !accumulate_only && s_begin == 0 &&
+             s_end == p->samples && chunk < PTG_BVH_HEAD_CHUNK && chunk < nsamp) {
+        const long long tslots = (long long)PTG_BVH_HEAD_TAIL_HALF_ROUNDS * ctx->wave_slots / 2;
+        int tail_rows = (int)((tslots + A.waves_per_row - 1) / A.waves_per_row);
+        if (tail_rows < A.slab_rows) {
+            const int hc = PTG_BVH_HEAD_CHUNK < nsamp ? PTG_BVH_HEAD_CHUNK : nsamp;
+            const int hn = (nsamp + hc - 1) / hc;
+            const int row = A.slab_rows - tail_rows;
+            A.lvl_chunk[0] = hc;
+            A.lvl_group[1] = row * A.waves_per_row;
+            A.lvl_unit[1] = (long long)A.lvl_group[1] * hn;
+            const int tc = PTG_BVH_TAIL_CHUNK > 0 ? (PTG_BVH_TAIL_CHUNK < nsamp ? PTG_BVH_TAIL_CHUNK : nsamp) : chunk;
+            const int tn = (nsamp + tc - 1) / tc;
+            A.lvl_chunk[1] = tc;
+            A.lvl_group[2] = groups;
+            A.lvl_unit[2] = A.lvl_unit[1] + (long long)(groups - A.lvl_group[1]) * tn;
+            A.n_levels = 2;
+            A.n_units = A.lvl_unit[2];
+        }
+    }
+#endif
     const int waves_per_block = (ctx->n > kLinearMax ? PTG_BVH_BLOCK : kBlock) / 64;
     grid = (int)((A.n_units + waves_per_block - 1) / waves_per_block);
 }

@@ -416,3 +416,22 @@ def test_shards_with_split_tail_are_exact():
     for y in (0, 1, H - 1):
         ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
         _check_equal(full[H - 1 - y], ref[H - 1 - y])
+
+
+def test_bvh_two_level_units_are_exact():
+    """A BVH frame below the split-tail threshold (fill_launch: e.g. an 8-way
+    shard of C5) runs its head rows in chunks of up to PTG_BVH_HEAD_CHUNK
+    samples and the last ~half round of rows in the auto chunk: the image
+    equals the same frame in explicit small chunks, and the oracle on a head
+    row and a tail row."""
+    _require_gpu()
+    W, H, samps = 1920, 160, 16
+    scn = ptgpu.make_scene("synthetic:300", W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    two, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    chunked, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1, chunk=3)
+    assert np.array_equal(two, chunked)
+    sp, ca = _oracle_scene(scn, cam)
+    for y in (0, H - 1):  # y = 0: the last slab row (tail level); H - 1: the first (head level)
+        ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
+        _check_equal(two[H - 1 - y], ref[H - 1 - y])
