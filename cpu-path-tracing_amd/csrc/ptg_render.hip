@@ -129,6 +129,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_TAIL_CHUNK
 #define PTG_BVH_TAIL_CHUNK 0  // ... in chunks of this many samples (0: the auto chunk, 20 at C5 8-way; 10: +0.8 %, 32: +5 %)
 #endif
+#ifndef PTG_DG_SKIP
+#define PTG_DG_SKIP 1  // shade: skip the diffuse/dielectric block when no lane of the wave needs it
+#endif
 #ifndef PTG_SMALL_DISC_SKIP
 #define PTG_SMALL_DISC_SKIP 1  // linear scan: skip a small sphere's root when no lane's disc >= 0 (box -0.9 %, box_mirror -2.1 %, simple -7 %; also skipping spheres behind every lane: +0.1-0.5 %)
 #endif
@@ -699,49 +702,56 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     const int mat = __float_as_int(s1.w);
     const bool isD = mat == PTG_DIFFUSE;
     const bool isG = mat == PTG_DIELECTRIC;
-    float cp = 0.0f, sp = 0.0f, ra = 0.0f;
-    if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
-        const uint32_t m_phi = draw_bits(st);
-        ra = draw(st);
-        sincos2pi_tab(m_phi, trig, cp, sp);
-    }
-    // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
-    f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
-    f3 v1 = isD ? uu : d;
-    const float r1 = rsqrt_d(dot3(v1, v1));
-    v1 = mk3(v1.x * r1, v1.y * r1, v1.z * r1);
-    const float x0 = -dot3(v1, nn);
-    const float cthG = 1.0f < x0 ? 1.0f : x0;  // main.cpp:77
-    // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
-    const float s2 = sqrt_d(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
-    const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
     bool spec = mat == PTG_SPECULAR;
-    if (isG) {
-        bool reflect = ratio * s2 > 1.0f;  // cannot refract: no Fresnel draw (main.cpp:89)
-        if (!reflect) {
-            const float r0 = 0x1.c71c74p-4f;  // ((1-ratio)/(1+ratio))^2, equal for ratio 0.5 and 2
-            float xm = 1.0f - cthG;
-            float x2 = xm * xm;
-            float x5 = (x2 * x2) * xm;
-            float R = __builtin_fmaf(1.0f - r0, x5, r0);
-            reflect = R > draw(st);
+    f3 nd = d;  // every lane sets it below (mirror lanes in the spec block)
+    // a wave with only mirror lanes skips the diffuse/dielectric work
+    // (wave-uniform, exact: those lanes' values are all overwritten)
+#if PTG_DG_SKIP
+    if (__ballot(isD | isG) != 0ull)
+#endif
+    {
+        float cp = 0.0f, sp = 0.0f, ra = 0.0f;
+        if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
+            const uint32_t m_phi = draw_bits(st);
+            ra = draw(st);
+            sincos2pi_tab(m_phi, trig, cp, sp);
         }
-        spec = reflect;
-    }
-    // op3: diffuse -> cos theta = sqrt(1 - r); dielectric -> |r_out_parallel| (main.cpp:94)
-    const f3 perp = mk3(__builtin_fmaf(nn.x, cthG, v1.x) * ratio, __builtin_fmaf(nn.y, cthG, v1.y) * ratio,
-                        __builtin_fmaf(nn.z, cthG, v1.z) * ratio);
-    const float s3 = sqrt_gs(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));  // both >= 0
-    f3 nd;
-    if (isD) {  // main.cpp:53-55 (unit by construction, not re-normalised)
-        f3 vv = cross3(nn, v1);
-        float cs = cp * s2, ss = sp * s2;
-        nd = mk3(__builtin_fmaf(nn.x, s3, __builtin_fmaf(vv.x, ss, v1.x * cs)),
-                 __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
-                 __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
-    } else {  // refraction, main.cpp:93-96
-        nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
-                 __builtin_fmaf(nn.z, -s3, perp.z));
+        // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
+        f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
+        f3 v1 = isD ? uu : d;
+        const float r1 = rsqrt_d(dot3(v1, v1));
+        v1 = mk3(v1.x * r1, v1.y * r1, v1.z * r1);
+        const float x0 = -dot3(v1, nn);
+        const float cthG = 1.0f < x0 ? 1.0f : x0;  // main.cpp:77
+        // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
+        const float s2 = sqrt_d(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
+        const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
+        if (isG) {
+            bool reflect = ratio * s2 > 1.0f;  // cannot refract: no Fresnel draw (main.cpp:89)
+            if (!reflect) {
+                const float r0 = 0x1.c71c74p-4f;  // ((1-ratio)/(1+ratio))^2, equal for ratio 0.5 and 2
+                float xm = 1.0f - cthG;
+                float x2 = xm * xm;
+                float x5 = (x2 * x2) * xm;
+                float R = __builtin_fmaf(1.0f - r0, x5, r0);
+                reflect = R > draw(st);
+            }
+            spec = reflect;
+        }
+        // op3: diffuse -> cos theta = sqrt(1 - r); dielectric -> |r_out_parallel| (main.cpp:94)
+        const f3 perp = mk3(__builtin_fmaf(nn.x, cthG, v1.x) * ratio, __builtin_fmaf(nn.y, cthG, v1.y) * ratio,
+                            __builtin_fmaf(nn.z, cthG, v1.z) * ratio);
+        const float s3 = sqrt_gs(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));  // both >= 0
+        if (isD) {  // main.cpp:53-55 (unit by construction, not re-normalised)
+            f3 vv = cross3(nn, v1);
+            float cs = cp * s2, ss = sp * s2;
+            nd = mk3(__builtin_fmaf(nn.x, s3, __builtin_fmaf(vv.x, ss, v1.x * cs)),
+                     __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
+                     __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
+        } else {  // refraction, main.cpp:93-96
+            nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
+                     __builtin_fmaf(nn.z, -s3, perp.z));
+        }
     }
     if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
         float k = dot3(on, d);
