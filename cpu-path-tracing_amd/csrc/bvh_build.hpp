@@ -246,12 +246,14 @@ inline int bvh_octant_mask(const BvhBuild &b)
     return mask;
 }
 
-inline BvhBuild build_bvh(const ptg_sphere *s, int n, double big_radius)
+// huge[i]: sphere i takes the anchored form (ptg_render.hip is_huge) and is
+// tested linearly, outside the tree
+inline BvhBuild build_bvh(const ptg_sphere *s, int n, const std::vector<char> &huge)
 {
     BvhBuild b;
     std::vector<int32_t> idx;
     for (int i = 0; i < n; ++i) {
-        if (s[i].radius >= big_radius)
+        if (huge[i])
             b.big.push_back(i);
         else
             idx.push_back(i);

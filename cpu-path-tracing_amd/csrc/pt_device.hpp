@@ -26,23 +26,28 @@ struct f3 {
 __device__ __forceinline__ f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ f3 sub3(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
-// Deterministic reciprocal square root: bit-trick seed + two Newton steps in
-// explicit fmaf (8 VALU ops instead of the ~28 of IEEE sqrt + division); the
-// oracle's rsqrt_B executes the same operations, so results agree bit for bit.
+// Deterministic reciprocal square root: bit-trick seed + three Newton steps
+// in explicit fmaf (11 VALU ops, ~1 ulp, instead of the ~28 of IEEE sqrt +
+// division); the oracle's rsqrt_B executes the same operations, so results
+// agree bit for bit.  (Two steps leave ~5e-6, about 40 ulp.)
 __device__ __forceinline__ float rsqrt_d(float x)
 {
     float y = __uint_as_float(0x5f375a86u - (__float_as_uint(x) >> 1));
-    float h = 0.5f * x;
-    float t = y * y;
-    t = __builtin_fmaf(-h, t, 1.5f);
-    y = y * t;
-    t = y * y;
-    t = __builtin_fmaf(-h, t, 1.5f);
-    return y * t;
+    const float h = 0.5f * x;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float t = y * y;
+        t = __builtin_fmaf(-h, t, 1.5f);
+        y = y * t;
+    }
+    return y;
 }
 // Deterministic square root for x >= 0 (x = +0 gives 0): the same bit-trick
-// seed y ~ 1/sqrt(x), then two coupled Goldschmidt steps on g ~ sqrt(x) and
-// h ~ 1/(2 sqrt(x)) -- 9 VALU, relative error ~1e-6, no special case for 0.
+// seed y ~ 1/sqrt(x), two coupled Goldschmidt steps on g ~ sqrt(x) and
+// h ~ 1/(2 sqrt(x)), then one Newton residual step g + (x - g^2) h -- 11 VALU,
+// within 1 ulp (0.63 measured), no special case for 0.  (The two steps alone
+// leave ~5e-6, about 40 ulp: after the discriminant form, the largest single
+// part of the fp32-vs-fp64 image difference, DESIGN.md "error budget".)
 // The oracle's sqrt_gs_B executes the same operations.
 __device__ __forceinline__ float sqrt_gs(float x)
 {
@@ -53,8 +58,11 @@ __device__ __forceinline__ float sqrt_gs(float x)
     g = __builtin_fmaf(g, r, g);
     h = __builtin_fmaf(h, r, h);
     r = __builtin_fmaf(-g, h, 0.5f);
-    return __builtin_fmaf(g, r, g);
+    g = __builtin_fmaf(g, r, g);
+    return __builtin_fmaf(__builtin_fmaf(-g, g, x), h, g);
 }
+// the scan's square root (ray-sphere discriminant): the same sequence
+__device__ __forceinline__ float sqrt_scan(float x) { return sqrt_gs(x); }
 // sqrt for any x: 0 for x <= 0 (the clamp as an integer max: negative floats
 // are negative integers; one VALU, no canonicalisation)
 __device__ __forceinline__ float sqrt_d(float x) { return sqrt_gs(__int_as_float(max(__float_as_int(x), 0))); }

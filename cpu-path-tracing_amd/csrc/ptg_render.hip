@@ -155,6 +155,20 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 template <bool kBvh>
 constexpr int kBlockOf = kBvh ? PTG_BVH_BLOCK : kBlock;
 constexpr double kBigRadius = 1000.0;
+// A sphere takes the anchored form ("huge", DESIGN.md "huge spheres") when its
+// radius is >= 1000 or more than 16 times the camera's distance to its
+// surface (+1): locally plane-like for the scene, where c = |o - C|^2 - R^2
+// cancels in fp32 (simple_scene's R = 100 ground: RMSE vs fp64 1.5e-3 ->
+// 3.3e-4).  The oracle's is_huge_B applies the same rule.
+inline bool is_huge(const ptg_sphere &sp, const ptg_camera *cam)
+{
+    if (sp.radius >= kBigRadius)
+        return true;
+    double d2 = 0.0;
+    for (int c = 0; c < 3; ++c)
+        d2 += (cam->position[c] - sp.position[c]) * (cam->position[c] - sp.position[c]);
+    return sp.radius > 16.0 * (std::fabs(std::sqrt(d2) - sp.radius) + 1.0);
+}
 
 struct KArgs {
     const LinRec *lin;      // linear scenes (<= kLinearMax): n records in scan order + sentinel
@@ -175,7 +189,7 @@ struct KArgs {
     // box mode (scan_order_of: every axis-anchored wall belongs to the one
     // pair or is the one single wall of its axis, at least one pair, no
     // other huge sphere): per axis the + and - walls' records (-1: none) and
-    // tangent planes (+-kFarPlane: none); pair_lo/hi bound the room on every
+    // tangent planes (+-inf: none); pair_lo/hi bound the room on every
     // axis (+-kFarPlane where open)
     int box_mode;
     int rec_plus[3], rec_minus[3];  // byte offsets of the records
@@ -219,6 +233,7 @@ struct KArgs {
     int sample_begin, sample_end;  // samples [begin, end) of every sub-pixel in this launch
     int keep_acc;                  // resolve without re-zeroing (progressive previews)
     int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
+    int count_nonfinite;           // PTG_FLAG_COUNT_NONFINITE: segments[3] += paths quant() would clip
     long long n_units;
     float *out;
     unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
@@ -288,7 +303,7 @@ __device__ __forceinline__ void camera_ray(const CamC &C, const Lane &L, uint32_
 // DESIGN.md "scene scan") are exact early-outs that never let a wave skip the
 // sqrt in practice, so they are left out here (-15 % frame time, same bits).
 constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
-constexpr float kFarPlane = 1e30f;             // box mode: the plane of a missing wall
+constexpr float kFarPlane = 1e30f;             // box mode: the room bound of an open side
 constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall skip test
 
 enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5 };
@@ -303,7 +318,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     const LinRec *best = recs + A.n;
-    auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f) {
+    auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
+                        const bool valid = true) {
         constexpr int kKind = decltype(kind_tag)::value;
         // r is wave-uniform, except for a pair's walls / box mode
         float4 g0 = r->g.g0;
@@ -327,9 +343,22 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
         } else {
             hb = ed;
-            c = ee + g1.w;
+            c = ee + g1.w;  // g1.w = -R^2
         }
-        const float disc = __builtin_fmaf(hb, hb, -(a * c));
+        float disc;
+        if constexpr (kKind == kSmall) {
+            // Lagrange's identity: hb^2 - a c = a R^2 - |e x d|^2.  hb^2 - a c
+            // cancels to ~1e-3 relative for a sphere of radius r at distance
+            // D >> r (two terms of size a D^2 for a difference of size a r^2);
+            // this form keeps the rounding at the scale of a r^2 (DESIGN.md
+            // "error budget": box_mirror 1920x1080x1024 RMSE vs fp64 1.9e-3 ->
+            // 5e-5).  Huge spheres keep hb^2 - a c: there the anchored hb, c
+            // are accurate and a R^2 would be ~1e12.
+            const f3 x = cross3(e, d);
+            disc = __builtin_fmaf(a, -g1.w, -dot3(x, x));
+        } else {
+            disc = __builtin_fmaf(hb, hb, -(a * c));
+        }
 #if PTG_SMALL_DISC_SKIP
         // a small sphere no lane's ray line meets cannot win: the wave skips
         // the root (exact: "win" below requires disc >= 0)
@@ -339,7 +368,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         }
 #endif
         // disc < 0 is rejected below whatever sq is: no clamp
-        const float sq = sqrt_gs(disc);
+        const float sq = sqrt_scan(disc);
         const bool neg = hb < 0.0f;
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
@@ -348,7 +377,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         const float den = (neg & near_lt) ? a : qq;
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
-        const bool win = !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
+        const bool win = valid & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
         bn = win ? num : bn;
         bq = win ? den : bq;
         best = win ? r : best;
@@ -400,8 +429,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             const float dk = comp(d, k);
             const bool pos = dk >= 0.0f;
             // (o - pm) is the same IEEE subtraction as -(pm - o).  A missing
-            // wall's plane is at +-kFarPlane: u ~ 1e30 is never the nearest
-            // and never needed below
+            // wall's plane is at +-inf: u = inf is never the nearest (inf * v
+            // is inf or NaN, and NaN compares false) and never needed below
             const float up = pp - comp(o, k), um = comp(o, k) - pm;
             u[k] = pos ? up : um;
             v[k] = __builtin_fabsf(dk);
@@ -414,13 +443,20 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             vn = nearer ? v[k] : vn;
             kn = nearer ? k : kn;
         }
+        // kn's wall is missing only when no existing wall the ray moves
+        // toward has v > 0 (every such plane is parallel to the ray): then no
+        // wall can be hit from inside the room, and the test is masked
         const int in = walls[2 * kn + (comp(d, kn) >= 0.0f ? 0 : 1)];
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
-        test_rec(rec_at(in), std::integral_constant<int, kAxAny>{}, un, vn);  // in >= 0: some axis has a pair
+        test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, kAxAny>{}, un, vn, in >= 0);
         const float bqm = bq * kPlaneMargin;
         bool need[3];
-        for (int k = 0; k < 3; ++k)
-            need[k] = (k != kn) & !(bn * v[k] < u[k] * bqm);
+        for (int k = 0; k < 3; ++k) {
+            // a missing wall is never needed (u = inf; also guarded by the
+            // uniform per-axis record flags)
+            const bool has = comp(d, k) >= 0.0f ? A.rec_plus[k] >= 0 : A.rec_minus[k] >= 0;
+            need[k] = (k != kn) & has & !(bn * v[k] < u[k] * bqm);
+        }
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             if (!in_room) {
                 for (; i < A.end_ax[0]; ++i)
@@ -483,16 +519,26 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
         c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
     } else {
         hb = ed;
-        c = ee + g0.w;
+        c = ee + g0.w;  // g0.w = -R^2
     }
     if (hb >= 0.0f && c >= 0.0f)
         return kReject;
     if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * kCullMargin)
         return kReject;  // near root > tb
-    float disc = __builtin_fmaf(hb, hb, -(a * c));
+    float disc;
+    if constexpr (kBig) {
+        disc = __builtin_fmaf(hb, hb, -(a * c));
+    } else {
+        // Lagrange form (scene_scan), limited to hb^2 for an origin outside
+        // (c >= 0: exactly disc <= hb^2), which keeps q <= 2|hb|(1 + 3u)
+        // and so the cull above exact
+        const f3 x = cross3(e, d);
+        disc = __builtin_fmaf(a, -g0.w, -dot3(x, x));
+        disc = c >= 0.0f ? __builtin_fminf(disc, hb * hb) : disc;
+    }
     if (disc < 0.0f)
         return kReject;
-    float sq = sqrt_gs(disc);  // disc >= 0 here
+    float sq = sqrt_scan(disc);  // disc >= 0 here
     float num, den;
     if (hb < 0.0f) {
         float q = sq - hb;
@@ -776,6 +822,10 @@ __device__ __forceinline__ int out_row_of(const KArgs &A, int slab_row)
 // trunc(c * 2^32) for c in [0, 2^30] without double arithmetic: integer part
 // and fraction * 2^32 are both exact in fp32, so this equals the oracle's
 // (uint64_t)((double)c * 0x1p32) bit for bit.
+// quant() is exact for c in [0, 2^30]; NaN and negative values become 0 and
+// larger ones 2^30 -- the counting kernel reports such paths
+// (PTG_FLAG_COUNT_NONFINITE), none are expected
+__device__ __forceinline__ bool in_quant_range(float c) { return c >= 0.0f && c <= 0x1p30f; }
 __device__ __forceinline__ unsigned long long quant(float c)
 {
     if (!(c >= 0.0f))
@@ -948,7 +998,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     }
     int next = total < 128 ? total : 128;  // wave-uniform pool cursor
     bool waiting = false;                  // path ended, no prefetched ray yet
+    uint32_t bad = 0;  // counting kernel: paths with a NaN / negative / > 2^30 radiance component
     auto flush = [&](float ex, float ey, float ez, int sl) {
+        if constexpr (kCount)
+            bad += (in_quant_range(ex) && in_quant_range(ey) && in_quant_range(ez)) ? 0u : 1u;
         atomicAdd(&lds_acc[wv][sl], quant(ex));
         atomicAdd(&lds_acc[wv][sl + 64], quant(ey));
         atomicAdd(&lds_acc[wv][sl + 128], quant(ez));
@@ -1098,12 +1151,15 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     if (parked)
         flush_parked();
     if constexpr (kCount) {
-        unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes;
+        unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes, wbad = bad;
         for (int off = 32; off > 0; off >>= 1) {
             ws += __shfl_xor(ws, off, 64);
             wsph += __shfl_xor(wsph, off, 64);
             wbox += __shfl_xor(wbox, off, 64);
+            wbad += __shfl_xor(wbad, off, 64);
         }
+        if (lane == 0 && A.count_nonfinite && wbad)
+            atomicAdd(A.segments + 3, wbad);
         if (lane == 0 && ws)
             atomicAdd(A.segments, ws);
         if (lane == 0 && A.count_tests) {
@@ -1246,6 +1302,7 @@ struct ptg_context {
     float2 *d_trig;  // sin/cos table (trig_table)
     unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
     size_t acc_elems;
+    bool acc_dirty;  // progressive sums may be in d_acc (accumulate / keep_acc resolve since the last reset)
     KArgs base;  // camera + scene fields filled
 };
 
@@ -1313,7 +1370,7 @@ SceneBox scene_box(const ptg_sphere *s, int n, const ptg_camera *cam)
     for (int c = 0; c < 3; ++c)
         b.lo[c] = b.hi[c] = cam->position[c];
     for (int i = 0; i < n; ++i) {
-        if (s[i].radius >= kBigRadius)
+        if (is_huge(s[i], cam))
             continue;
         for (int c = 0; c < 3; ++c) {
             b.lo[c] = std::min(b.lo[c], s[i].position[c] - s[i].radius);
@@ -1341,7 +1398,7 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
         const ptg_sphere &sp = s[i];
         const double R = sp.radius;
         GeoRec g;
-        if (R >= kBigRadius) {
+        if (is_huge(sp, cam)) {
             double P[3], N[3];
             axis[i] = choose_anchor(sp, cam, box, P, N);
             g.g0 = make_float4((float)P[0], (float)P[1], (float)P[2], (float)R);
@@ -1385,8 +1442,27 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
 // plane) keep the rule; pair_lo/hi are those bounds rounded to float.  The
 // oracle's prep_B forms the same pairs (pt_oracle.c).  plus[k] / minus[k] =
 // scene index or -1.
+// A wall may take part in wall pairs / box mode only if no ray origin can lie
+// genuinely inside it, beyond its tangent plane, where the "test only the
+// wall the ray moves toward" rule would drop a hit of the wall from inside:
+// the wall is not dielectric (no path is transmitted into it) and the camera
+// is on the room side by more than the margin.  Other spheres need no check:
+// a sphere sunk into the wall has its sunk part inside the wall, which a ray
+// from the room reaches only through the wall's surface -- the wall is hit
+// there first (tests/test_scene_file.py: a glass sphere sunk into a wall,
+// pairs on vs every sphere tested, same image).  The oracle's wall_clear_B
+// makes the same choice.
+bool wall_clear(const ptg_sphere *s, int i, int k, bool plus_side, const ptg_camera *cam, const SceneBox &box)
+{
+    if (s[i].material == PTG_DIELECTRIC)
+        return false;
+    const double margin = 1e-4 * std::max(1.0, box.diag);
+    const double a = plus_side ? s[i].position[k] - s[i].radius : s[i].position[k] + s[i].radius;
+    return plus_side ? cam->position[k] < a - margin : cam->position[k] > a + margin;
+}
+
 void pair_walls(const ptg_sphere *s, int n, const std::vector<int> &axis, const std::vector<GeoRec> &geo,
-                const SceneBox &box, int plus[3], int minus[3], float lo[3], float hi[3])
+                const ptg_camera *cam, const SceneBox &box, int plus[3], int minus[3], float lo[3], float hi[3])
 {
     const double margin = 1e-4 * std::max(1.0, box.diag);
     for (int k = 0; k < 3; ++k) {
@@ -1400,7 +1476,8 @@ void pair_walls(const ptg_sphere *s, int n, const std::vector<int> &axis, const 
             if (nk > 0.0f && minus[k] < 0)
                 minus[k] = i;
         }
-        if (plus[k] < 0 || minus[k] < 0) {
+        if (plus[k] < 0 || minus[k] < 0 || !wall_clear(s, plus[k], k, true, cam, box) ||
+            !wall_clear(s, minus[k], k, false, cam, box)) {
             plus[k] = minus[k] = -1;
             lo[k] = hi[k] = 0.0f;
             continue;
@@ -1425,7 +1502,7 @@ void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::v
     A.box_mode = 0;
     int cnt[3] = {0, 0, 0}, general = 0;
     for (int i = 0; i < n; ++i) {
-        if (s[i].radius < kBigRadius)
+        if (!is_huge(s[i], cam))
             continue;
         if (axis[i] < 0)
             ++general;
@@ -1435,14 +1512,17 @@ void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::v
     bool ok = general == 0 && (A.pairs[0] || A.pairs[1] || A.pairs[2]);
     for (int k = 0; k < 3; ++k)
         ok = ok && (A.pairs[k] ? cnt[k] == 2 : cnt[k] <= 1);
+    const SceneBox box = scene_box(s, n, cam);
+    for (int i = 0; i < n && ok; ++i)  // single walls too (the pairs' members are clear)
+        if (is_huge(s[i], cam) && axis[i] >= 0)
+            ok = wall_clear(s, i, axis[i], (&geo[i].g1.x)[axis[i]] < 0.0f, cam, box);
     if (!ok)
         return;
-    const SceneBox box = scene_box(s, n, cam);
     const double margin = 1e-4 * std::max(1.0, box.diag);
     for (int k = 0; k < 3; ++k) {
         A.rec_plus[k] = A.rec_minus[k] = -1;
-        A.plane_plus[k] = kFarPlane;
-        A.plane_minus[k] = -kFarPlane;
+        A.plane_plus[k] = HUGE_VALF;  // missing wall: never the nearest plane, never needed
+        A.plane_minus[k] = -HUGE_VALF;
         const int begin = k == 0 ? 0 : A.end_ax[k - 1];
         for (int j = begin; j < A.end_ax[k]; ++j) {
             const int i = order[j];
@@ -1477,7 +1557,7 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam
 {
     std::vector<int> order;
     int plus[3], minus[3];
-    pair_walls(s, n, axis, geo, scene_box(s, n, cam), plus, minus, A.pair_lo, A.pair_hi);
+    pair_walls(s, n, axis, geo, cam, scene_box(s, n, cam), plus, minus, A.pair_lo, A.pair_hi);
     for (int k = 0; k < 3; ++k) {
         A.pairs[k] = plus[k] >= 0 ? 1 : 0;
         if (A.pairs[k]) {
@@ -1491,11 +1571,11 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam
     }
     box_mode_of(s, n, cam, axis, geo, order, A);
     for (int i = 0; i < n; ++i)
-        if (s[i].radius >= kBigRadius && axis[i] < 0)
+        if (is_huge(s[i], cam) && axis[i] < 0)
             order.push_back(i);
     A.end_big = (int)order.size();
     for (int i = 0; i < n; ++i)
-        if (s[i].radius < kBigRadius)
+        if (!is_huge(s[i], cam))
             order.push_back(i);
     return order;
 }
@@ -1538,8 +1618,8 @@ int check_params(const ptg_params *p)
 }
 
 // Launch geometry for samples [s_begin, s_end) of every sub-pixel.
-void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid, int s_begin = 0, int s_end = -1,
-                 bool accumulate_only = false)
+int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid, int s_begin = 0, int s_end = -1,
+                bool accumulate_only = false)
 {
     if (s_end < 0)
         s_end = p->samples;
@@ -1567,6 +1647,7 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     A.sample_end = s_end;
     A.keep_acc = 0;
     A.count_tests = (p->flags & PTG_FLAG_COUNT_TESTS) != 0;
+    A.count_nonfinite = (p->flags & PTG_FLAG_COUNT_NONFINITE) != 0;
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
@@ -1670,7 +1751,13 @@ void fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &gri
     }
 #endif
     const int waves_per_block = (ctx->n > kLinearMax ? PTG_BVH_BLOCK : kBlock) / 64;
-    grid = (int)((A.n_units + waves_per_block - 1) / waves_per_block);
+    const long long g = (A.n_units + waves_per_block - 1) / waves_per_block;  // 64-bit before any cast
+    grid = 0;
+    if (g > 0x7FFFFFFFLL)
+        return fail(PTG_ERR_UNSUPPORTED, "too many work units (" + std::to_string(A.n_units) +
+                                             "): raise chunk_samples or use 0 (auto)");
+    grid = (int)g;
+    return PTG_OK;
 }
 
 int set_device(int device)
@@ -1793,7 +1880,10 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
     A.end_big = order.end_big;
     if ((int)n_spheres > kLinearMax) {
-        BvhBuild b = build_bvh(spheres, (int)n_spheres, kBigRadius);
+        std::vector<char> huge(n_spheres);
+        for (size_t i = 0; i < n_spheres; ++i)
+            huge[i] = is_huge(spheres[i], cam);
+        BvhBuild b = build_bvh(spheres, (int)n_spheres, huge);
         std::vector<BvhNodeQ> qn;
         const BvhGrid grid = quantise_bvh(b.nodes, qn);
         const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();
@@ -1933,6 +2023,7 @@ int ensure_acc(ptg_context *ctx, size_t need)
         return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the accumulator failed");
     PTG_HIP(hipMemset(ctx->d_acc, 0, need * sizeof(unsigned long long)));
     ctx->acc_elems = need;
+    ctx->acc_dirty = false;  // (a progressive frame in the old buffer is lost: reset before reuse)
     return PTG_OK;
 }
 
@@ -1979,7 +2070,8 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
-    fill_launch(ctx, params, A, grid);
+    if ((rc = fill_launch(ctx, params, A, grid)))
+        return rc;
     // several units per pixel, a split tail, or no samples at all
     const bool resolve = !A.single_chunk || A.n_levels > 1 || grid == 0;
     if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
@@ -1988,6 +2080,12 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     A.acc = ctx->d_acc;
     A.segments = d_segments;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (resolve && ctx->acc_dirty) {
+        // progressive sums left by accumulate / keep_acc resolve: a one-shot
+        // frame starts from zero (its resolve leaves the buffer zero again)
+        PTG_HIP(hipMemsetAsync(ctx->d_acc, 0, ctx->acc_elems * sizeof(unsigned long long), s));
+        ctx->acc_dirty = false;
+    }
     if ((rc = launch_render(A, grid, d_segments != nullptr, s)))
         return rc;
     return resolve ? launch_resolve(A, s) : PTG_OK;
@@ -2006,11 +2104,13 @@ int ptg_accumulate_device(ptg_context *ctx, const ptg_params *params, int32_t sa
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
-    fill_launch(ctx, params, A, grid, sample_begin, sample_end, /*accumulate_only=*/true);
+    if ((rc = fill_launch(ctx, params, A, grid, sample_begin, sample_end, /*accumulate_only=*/true)))
+        return rc;
     if ((rc = ensure_acc(ctx, acc_elems_for(A))))
         return rc;
     A.acc = ctx->d_acc;
     A.segments = d_segments;
+    ctx->acc_dirty = true;
     return launch_render(A, grid, d_segments != nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -2026,7 +2126,8 @@ int ptg_resolve_device(ptg_context *ctx, const ptg_params *params, int32_t sampl
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
-    fill_launch(ctx, params, A, grid);
+    if ((rc = fill_launch(ctx, params, A, grid)))
+        return rc;
     if ((rc = ensure_acc(ctx, acc_elems_for(A))))
         return rc;
     A.samps = samples_done;  // mean over the samples accumulated so far
@@ -2047,11 +2148,13 @@ int ptg_reset_accumulation_device(ptg_context *ctx, const ptg_params *params, vo
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
-    fill_launch(ctx, params, A, grid);
+    if ((rc = fill_launch(ctx, params, A, grid)))
+        return rc;
     if ((rc = ensure_acc(ctx, acc_elems_for(A))))
         return rc;
-    PTG_HIP(hipMemsetAsync(ctx->d_acc, 0, acc_elems_for(A) * sizeof(unsigned long long),
+    PTG_HIP(hipMemsetAsync(ctx->d_acc, 0, ctx->acc_elems * sizeof(unsigned long long),
                            reinterpret_cast<hipStream_t>(stream)));
+    ctx->acc_dirty = false;
     return PTG_OK;
 }
 
@@ -2068,7 +2171,8 @@ int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const i
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
-    fill_launch(ctx, params, A, grid);
+    if ((rc = fill_launch(ctx, params, A, grid)))
+        return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int blocks = (int)((n + kTraceBlock - 1) / kTraceBlock);
     if (A.n > kLinearMax)

@@ -45,6 +45,11 @@ def _camera_array(cam) -> np.ndarray:
 
 
 FLAG_COUNT_TESTS = 1  # include/ptgpu.h PTG_FLAG_COUNT_TESTS
+FLAG_COUNT_NONFINITE = 2  # include/ptgpu.h PTG_FLAG_COUNT_NONFINITE (4 counters)
+
+
+def _n_counters(flags: int) -> int:
+    return 4 if flags & FLAG_COUNT_NONFINITE else (3 if flags & FLAG_COUNT_TESTS else 1)
 
 
 def make_params(width, height, samples, num_subpixels=2, seed=DEFAULT_SEED, band_rows=DEFAULT_BAND_ROWS,
@@ -121,6 +126,21 @@ class Context:
                                        -1 if device is None else int(device), C.byref(h)), "ptg_context_create")
         self._h = h
         self.n_spheres = len(sp)
+        if device is None or int(device) < 0:
+            import torch
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        self.device = int(device)
+
+    def _stream(self, stream):
+        """The HIP stream handle: `stream`, or torch's current stream on the
+        context's device (not the current device)."""
+        import torch
+        return (stream or torch.cuda.current_stream(torch.device("cuda", self.device))).cuda_stream
+
+    def _check(self, t, dtype, min_numel):
+        _check_tensor(t, dtype, min_numel)
+        if t.device.index != self.device:
+            raise ValueError(f"tensor on {t.device}, context on cuda:{self.device}")
 
     def close(self):
         if self._h:
@@ -144,25 +164,26 @@ class Context:
         shard_rows*W*3 values) on `stream` (torch.cuda.Stream or None =
         torch's current stream)."""
         import torch
-        _check_tensor(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
-                      * params.width * 3)
+        self._check(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
+                    * params.width * 3)
         if segments is not None:
-            _check_tensor(segments, torch.int64, 3 if params.flags & FLAG_COUNT_TESTS else 1)
-        s = (stream or torch.cuda.current_stream(out.device)).cuda_stream
+            self._check(segments, torch.int64, _n_counters(params.flags))
+        s = self._stream(stream)
         check(lib().ptg_render_device(self._h, C.byref(params), C.c_void_p(out.data_ptr()),
                                       C.c_void_p(segments.data_ptr()) if segments is not None else None,
                                       C.c_void_p(s)), "ptg_render_device")
 
     # ---- progressive accumulation (ptg_accumulate_device / ptg_resolve_device)
     def reset_accumulation(self, params: Params, stream=None) -> None:
-        import torch
-        s = (stream or torch.cuda.current_stream()).cuda_stream
+        s = self._stream(stream)
         check(lib().ptg_reset_accumulation_device(self._h, C.byref(params), C.c_void_p(s)), "ptg_reset_accumulation_device")
 
     def accumulate(self, params: Params, sample_begin: int, sample_end: int, segments=None, stream=None) -> None:
         """Add samples [sample_begin, sample_end) of every sub-pixel."""
         import torch
-        s = (stream or torch.cuda.current_stream()).cuda_stream
+        if segments is not None:
+            self._check(segments, torch.int64, _n_counters(params.flags))
+        s = self._stream(stream)
         check(lib().ptg_accumulate_device(self._h, C.byref(params), int(sample_begin), int(sample_end),
                                           C.c_void_p(segments.data_ptr()) if segments is not None else None,
                                           C.c_void_p(s)), "ptg_accumulate_device")
@@ -170,9 +191,9 @@ class Context:
     def resolve(self, out, params: Params, samples_done: int, stream=None) -> None:
         """Preview/final image from the samples accumulated so far."""
         import torch
-        _check_tensor(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
-                      * params.width * 3)
-        s = (stream or torch.cuda.current_stream(out.device)).cuda_stream
+        self._check(out, torch.float32, shard_rows(params.height, params.band_rows, params.shard_count)
+                    * params.width * 3)
+        s = self._stream(stream)
         check(lib().ptg_resolve_device(self._h, C.byref(params), int(samples_done), C.c_void_p(out.data_ptr()),
                                        C.c_void_p(s)), "ptg_resolve_device")
 
@@ -180,11 +201,14 @@ class Context:
         """Parity probe: radiance + segment count of individual paths
         (coords: int32 CUDA tensor [n, 5] = x, y, sx, sy, sample)."""
         import torch
+        if coords.dim() != 2 or coords.shape[1] != 5:
+            raise ValueError("coords must be [n, 5] (x, y, sx, sy, sample)")
+        coords = coords.contiguous()
+        self._check(coords, torch.int32, coords.numel())
         n = coords.shape[0]
         out = torch.empty((n, 3), dtype=torch.float32, device=coords.device)
         segs = torch.empty((n,), dtype=torch.int32, device=coords.device)
-        coords = coords.contiguous()
-        s = torch.cuda.current_stream(coords.device).cuda_stream
+        s = self._stream(None)
         check(lib().ptg_trace_samples_device(self._h, C.byref(params), C.c_void_p(coords.data_ptr()), n,
                                              C.c_void_p(out.data_ptr()), C.c_void_p(segs.data_ptr()),
                                              C.c_void_p(s)), "ptg_trace_samples_device")

@@ -89,6 +89,11 @@ typedef struct ptg_params {
  * ptg_accumulate_device points to 3 counters: += scene scans, sphere tests
  * (ray-sphere quadratics), BVH box tests -- the inputs of the roofline model. */
 #define PTG_FLAG_COUNT_TESTS 1
+/* with PTG_FLAG_COUNT_NONFINITE (implies the counters above), d_segments points
+ * to 4 counters; the 4th += paths whose radiance has a component that is NaN,
+ * negative or above 2^30 -- values the exact accumulation would clip (NaN and
+ * negative to 0).  None are expected: the -m gpu tests assert 0. */
+#define PTG_FLAG_COUNT_NONFINITE 2
 
 typedef struct ptg_context ptg_context;
 

@@ -524,32 +524,67 @@ int po_render_xs_f64(const po_sphere *s, int n, const po_camera *cam, int W, int
 #define EPSF 1e-4f
 #define INFF 1e20f
 
+/* Mode B' (error decomposition, tests/test_error_budget.py): each flag swaps one
+ * of Mode B's deliberate approximations for the accurate fp32 operation, so the
+ * fp32-vs-fp64 difference can be split into "approximations" and "fp32 as
+ * such".  0 = Mode B (the GPU's op sequence). */
+#define PO_BV_IEEE_SQRT 1   /* sqrtf / 1.0f/sqrtf instead of the Newton/Goldschmidt sequences */
+#define PO_BV_IEEE_DIV 2    /* n / d instead of the Newton reciprocal */
+#define PO_BV_LIBM_TRIG 4   /* (float)cos/sin(2 pi u) in double instead of the table */
+#define PO_BV_RENORM 8      /* normal = norm(p - C), diffuse direction re-normalised (main.cpp:55) */
+#define PO_BV_FULL_SCAN 16  /* every sphere tested in index order (no wall pairs / box mode) */
+#define PO_BV_LEX 32        /* every candidate divided, lowest index wins ties (main.cpp:35) */
+#define PO_BV_DISC_NAIVE 64 /* small spheres' discriminant as hb^2 - a c (round 1) instead of a R^2 - |e x d|^2 */
+static int g_bvar = 0;
+void po_set_mode_b_variant(int flags) { g_bvar = flags; }
+int po_get_mode_b_variant(void) { return g_bvar; }
+/* Anchored ("huge") form: R >= 1000, or R more than 16 times the camera's
+ * distance to the surface (+1).  The kernel's host side: ptg_render.hip
+ * is_huge. */
+static int is_huge_B(const po_sphere *sp, const po_camera *cam)
+{
+    if (sp->radius >= BIG_RADIUS)
+        return 1;
+    double d2 = 0.0;
+    for (int c = 0; c < 3; ++c)
+        d2 += (cam->position[c] - sp->position[c]) * (cam->position[c] - sp->position[c]);
+    return sp->radius > 16.0 * (fabs(sqrt(d2) - sp->radius) + 1.0);
+}
+
 typedef struct { float x, y, z; } f3;
 static f3 fk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static float fcomp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 static float fdot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 /* Deterministic reciprocal square root (DESIGN.md "fp32 math"): bit-trick seed
  * + two Newton steps written with explicit fmaf, so CPU and GPU agree bit for
  * bit; about 2 ulp, x > 0. */
 static float rsqrt_B(float x)
 {
+    if (g_bvar & PO_BV_IEEE_SQRT)
+        return 1.0f / sqrtf(x);
     uint32_t i;
     memcpy(&i, &x, 4);
     i = 0x5f375a86u - (i >> 1);
     float y;
     memcpy(&y, &i, 4);
     float h = 0.5f * x;
-    float t = y * y;
-    t = fmaf(-h, t, 1.5f);
-    y = y * t;
-    t = y * y;
-    t = fmaf(-h, t, 1.5f);
-    return y * t;
+    for (int k = 0; k < 3; ++k) { /* three Newton steps: ~1.7 ulp (two left ~5e-6, 40 ulp) */
+        float t = y * y;
+        t = fmaf(-h, t, 1.5f);
+        y = y * t;
+    }
+    return y;
 }
 /* Deterministic square root for x >= 0 (x = +0 gives 0): the rsqrt_B seed,
- * then two coupled Goldschmidt steps on g ~ sqrt(x), h ~ 1/(2 sqrt(x)).
- * Kernel: pt_device.hpp sqrt_gs. */
+ * two coupled Goldschmidt steps on g ~ sqrt(x), h ~ 1/(2 sqrt(x)), then one
+ * Newton residual step g + (x - g^2) h -- within 1 ulp (0.63 ulp measured;
+ * the two steps alone leave ~5e-6, about 40 ulp, which was the largest
+ * single part of the fp32-vs-fp64 image difference after the discriminant
+ * form: DESIGN.md "error budget").  Kernel: pt_device.hpp sqrt_gs. */
 static float sqrt_gs_B(float x)
 {
+    if (g_bvar & PO_BV_IEEE_SQRT)
+        return sqrtf(x);
     uint32_t i;
     memcpy(&i, &x, 4);
     i = 0x5f375a86u - (i >> 1);
@@ -561,8 +596,11 @@ static float sqrt_gs_B(float x)
     g = fmaf(g, r, g);
     h = fmaf(h, r, h);
     r = fmaf(-g, h, 0.5f);
-    return fmaf(g, r, g);
+    g = fmaf(g, r, g);
+    return fmaf(fmaf(-g, g, x), h, g);
 }
+/* the scan's square root (the discriminant): the same sequence */
+static float sqrt_scan_B(float x) { return sqrt_gs_B(x); }
 /* sqrt for any x: 0 for x <= 0 (clamped as an integer max, like the kernel) */
 static float sqrt_B(float x)
 {
@@ -576,6 +614,8 @@ static float sqrt_B(float x)
  * one residual correction of the quotient.  Kernel: pt_device.hpp div_d. */
 static float div_B(float n, float d)
 {
+    if (g_bvar & PO_BV_IEEE_DIV)
+        return n / d;
     uint32_t i;
     memcpy(&i, &d, 4);
     i = 0x7EF311C3u - i;
@@ -663,7 +703,7 @@ static boxB scene_box_B(const po_sphere *s, int n, const po_camera *cam)
     for (int c = 0; c < 3; ++c)
         b.lo[c] = b.hi[c] = cam->position[c];
     for (int i = 0; i < n; ++i) {
-        if (s[i].radius >= BIG_RADIUS)
+        if (is_huge_B(&s[i], cam))
             continue;
         for (int c = 0; c < 3; ++c) {
             double a = s[i].position[c] - s[i].radius, e = s[i].position[c] + s[i].radius;
@@ -686,7 +726,19 @@ static void trig_table_B(float *tab);
  * tangent planes x_k = a_minus, a_plus widened by 1e-4 max(1, diagonal)) tests
  * only the wall it moves toward (d_k >= 0: the + wall): each sphere lies
  * entirely beyond its tangent plane. */
-static void pair_walls_B(const po_sphere *s, int n, const boxB *box, sphB *out)
+/* A wall may be paired / take part in box mode only if no ray origin can lie
+ * genuinely inside it (the kernel's host side: ptg_render.hip wall_clear): not
+ * dielectric, the camera on the room side by more than the margin. */
+static int wall_clear_B(const po_sphere *s, int i, int k, int plus_side, const po_camera *cam, const boxB *box)
+{
+    if (s[i].material == 2)
+        return 0;
+    const double margin = 1e-4 * (box->diag > 1.0 ? box->diag : 1.0);
+    const double a = plus_side ? s[i].position[k] - s[i].radius : s[i].position[k] + s[i].radius;
+    return plus_side ? cam->position[k] < a - margin : cam->position[k] > a + margin;
+}
+
+static void pair_walls_B(const po_sphere *s, int n, const po_camera *cam, const boxB *box, sphB *out)
 {
     const double margin = 1e-4 * (box->diag > 1.0 ? box->diag : 1.0);
     for (int k = 0; k < 3; ++k) {
@@ -700,7 +752,8 @@ static void pair_walls_B(const po_sphere *s, int n, const boxB *box, sphB *out)
             if (nk > 0.0f && minus < 0)
                 minus = i;
         }
-        if (plus < 0 || minus < 0)
+        if (plus < 0 || minus < 0 || !wall_clear_B(s, plus, k, 1, cam, box) ||
+            !wall_clear_B(s, minus, k, 0, cam, box))
             continue;
         out[plus].pair = 1;
         out[minus].pair = -1;
@@ -714,7 +767,7 @@ static void pair_walls_B(const po_sphere *s, int n, const boxB *box, sphB *out)
  * only wall of its axis, some axis has a pair, no other huge sphere.  A
  * single wall's room bound (margin as pair_walls_B) goes into its own
  * plo (- side wall) or phi (+ side wall). */
-static void box_mode_B(const po_sphere *s, int n, const boxB *box, sphB *out)
+static void box_mode_B(const po_sphere *s, int n, const po_camera *cam, const boxB *box, sphB *out)
 {
     int cnt[3] = {0, 0, 0}, pairs[3] = {0, 0, 0}, general = 0;
     for (int i = 0; i < n; ++i) {
@@ -731,6 +784,9 @@ static void box_mode_B(const po_sphere *s, int n, const boxB *box, sphB *out)
     int ok = general == 0 && (pairs[0] || pairs[1] || pairs[2]);
     for (int k = 0; k < 3; ++k)
         ok = ok && (pairs[k] ? cnt[k] == 2 : cnt[k] <= 1);
+    for (int i = 0; i < n && ok; ++i) /* single walls too (the pairs' members are clear) */
+        if (out[i].big && out[i].axis >= 0)
+            ok = wall_clear_B(s, i, out[i].axis, fcomp(out[i].N, out[i].axis) < 0.0f, cam, box);
     if (!ok)
         return;
     const double margin = 1e-4 * (box->diag > 1.0 ? box->diag : 1.0);
@@ -754,7 +810,7 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         const po_sphere *sp = &s[i];
         sphB *b = &out[i];
         double R = sp->radius;
-        b->big = R >= BIG_RADIUS;
+        b->big = is_huge_B(sp, cam);
         b->R = (float)R;
         b->R2x = (float)(2.0 * R);
         b->negR2 = (float)(-(R * R));
@@ -792,8 +848,8 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
      * led by its wall pair, + wall first), the other huge spheres, the small
      * ones; each group otherwise in index order */
     if (n <= LINEAR_MAX_PREP) {
-        pair_walls_B(s, n, &box, out);
-        box_mode_B(s, n, &box, out);
+        pair_walls_B(s, n, cam, &box, out);
+        box_mode_B(s, n, cam, &box, out);
         int j = 0;
         for (int k = 0; k < 3; ++k) {
             for (int i = 0; i < n; ++i)
@@ -836,6 +892,12 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
 
 static void sincos2pi_B(uint32_t m, const float *tab, float *c, float *s)
 {
+    if (g_bvar & PO_BV_LIBM_TRIG) {
+        const double a = 2.0 * PO_PI * ((double)m * 0x1p-24);
+        *c = (float)cos(a);
+        *s = (float)sin(a);
+        return;
+    }
     const float *cs = tab + 2 * (m >> (24 - TRIG_BITS));
     float dl = (float)(m & ((1u << (24 - TRIG_BITS)) - 1u)) * 0x1.921fb6p-22f;
     float d2 = dl * dl;
@@ -896,13 +958,18 @@ static void test_B(const sphB *sp, int i, f3 o, f3 d, float a, float *bn, float 
         c = ee + sp->negR2;
     }
     if (hb >= 0.0f && c >= 0.0f)
-        return; /* both roots <= 0 */
-    if (hb < 0.0f && c > 0.0f && c * *bq >= (*bn * (-2.0f * hb)) * CULL_MARGIN)
-        return; /* near root provably not nearer than bn/bq */
+        return; /* both roots <= 0: num = -c <= 0 is rejected below (exact) */
+    /* small spheres: Lagrange's identity hb^2 - a c = a R^2 - |e x d|^2
+     * (no cancellation between two terms of size a|e|^2); the kernel's
+     * scene_scan, DESIGN.md "error budget" */
     float disc = fmaf(hb, hb, -(a * c));
+    if (!sp->big && !(g_bvar & PO_BV_DISC_NAIVE)) {
+        f3 x = fcross(e, d);
+        disc = fmaf(a, -sp->negR2, -fdot(x, x));
+    }
     if (disc < 0.0f)
         return;
-    float sq = sqrt_gs_B(disc); /* disc >= 0 here */
+    float sq = sqrt_scan_B(disc); /* disc >= 0 here */
     float num, den;
     if (hb < 0.0f) {
         float q = sq - hb; /* > 0; roots c/q (near) and q/a (far) */
@@ -930,7 +997,6 @@ static void test_B(const sphB *sp, int i, f3 o, f3 d, float a, float *bn, float 
 
 #define FAR_PLANE 1e30f
 #define PLANE_MARGIN 0x1.ffep-1f /* 1 - 2^-12 */
-static float fcomp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
 /* Box mode walls (the kernel's scene_scan): the wall of the nearest tangent
  * plane the ray moves toward first; another wall only where its plane is not
@@ -939,7 +1005,8 @@ static float fcomp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 static int box_walls_B(const sphB *s, int n, f3 o, f3 d, float a, float *bn, float *bq, int *id)
 {
     int rec_plus[3] = {-1, -1, -1}, rec_minus[3] = {-1, -1, -1};
-    float plane_plus[3] = {FAR_PLANE, FAR_PLANE, FAR_PLANE}, plane_minus[3] = {-FAR_PLANE, -FAR_PLANE, -FAR_PLANE};
+    /* a missing wall's plane is at +-inf: never the nearest, never needed */
+    float plane_plus[3] = {INFINITY, INFINITY, INFINITY}, plane_minus[3] = {-INFINITY, -INFINITY, -INFINITY};
     float lo[3] = {-FAR_PLANE, -FAR_PLANE, -FAR_PLANE}, hi[3] = {FAR_PLANE, FAR_PLANE, FAR_PLANE};
     int nw = 0;
     while (nw < n && s[s[nw].visit].big && s[s[nw].visit].axis >= 0) { /* the walls lead the scan order */
@@ -982,11 +1049,14 @@ static int box_walls_B(const sphB *s, int n, f3 o, f3 d, float a, float *bn, flo
             in = ci[k];
             kn = k;
         }
-    test_B(&s[in], in, o, d, a, bn, bq, id);
+    /* in < 0 only when no existing wall the ray moves toward has v > 0: no
+     * wall can be hit from inside the room (the kernel masks the test) */
+    if (in >= 0)
+        test_B(&s[in], in, o, d, a, bn, bq, id);
     const float bqm = *bq * PLANE_MARGIN;
     int need[3];
-    for (int k = 0; k < 3; ++k)
-        need[k] = k != kn && !(*bn * v[k] < u[k] * bqm); /* a missing wall: u ~ 1e30, never needed */
+    for (int k = 0; k < 3; ++k) /* a missing wall: u = inf, never needed; guarded as well */
+        need[k] = k != kn && ci[k] >= 0 && !(*bn * v[k] < u[k] * bqm);
     if (!in_room) {
         for (int j = 0; j < nw; ++j)
             test_B(&s[s[j].visit], s[j].visit, o, d, a, bn, bq, id);
@@ -1006,6 +1076,13 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
     float bn = INFF, bq = 1.0f;
     int id = -1;
     int j0 = 0;
+    if (g_bvar & PO_BV_FULL_SCAN) {
+        for (int i = 0; i < n; ++i)
+            test_B(&s[i], i, o, d, a, &bn, &bq, &id);
+        *tout = id >= 0 ? div_B(bn, bq) : INFF;
+        *idout = id;
+        return id >= 0;
+    }
     if (n > 0 && s[0].box)
         j0 = box_walls_B(s, n, o, d, a, &bn, &bq, &id);
     for (int j = j0; j < n; ++j) {
@@ -1055,9 +1132,16 @@ static int intersect_B_lex(const sphB *s, int n, f3 o, f3 d, float *tout, int *i
         if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * CULL_MARGIN)
             continue;
         float disc = fmaf(hb, hb, -(a * c));
+        if (!sp->big && !(g_bvar & PO_BV_DISC_NAIVE)) {
+            /* Lagrange form, limited to hb^2 for an origin outside (c >= 0:
+             * exactly disc <= hb^2) so that the cull above stays exact */
+            f3 x = fcross(e, d);
+            disc = fmaf(a, -sp->negR2, -fdot(x, x));
+            disc = c >= 0.0f ? fminf(disc, hb * hb) : disc;
+        }
         if (disc < 0.0f)
             continue;
-        float sq = sqrt_gs_B(disc);
+        float sq = sqrt_scan_B(disc);
         float num, den;
         if (hb < 0.0f) {
             float q = sq - hb;
@@ -1116,7 +1200,8 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y
         float t;
         int id;
         (*segs)++;
-        if (!(n > LINEAR_MAX ? intersect_B_lex(s, n, o, d, &t, &id) : intersect_B(s, n, o, d, &t, &id))) {
+        if (!(n > LINEAR_MAX || (g_bvar & PO_BV_LEX) ? intersect_B_lex(s, n, o, d, &t, &id)
+                                                     : intersect_B(s, n, o, d, &t, &id))) {
             f3 ud = fnorm(d);
             float tt = 0.5f * (ud.y + 1.0f);
             float it = 1.0f - tt;
@@ -1128,6 +1213,8 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y
         f3 p = fk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z));
         /* hit_record.cpp:6: (p - C).norm(), as (p - C) * (1/R): p lies on the sphere */
         f3 on = fk((p.x - sp->C.x) * sp->invR, (p.y - sp->C.y) * sp->invR, (p.z - sp->C.z) * sp->invR);
+        if (g_bvar & PO_BV_RENORM)
+            on = fnorm(fk(p.x - sp->C.x, p.y - sp->C.y, p.z - sp->C.z));
         int front = fdot(on, d) < 0.0f;
         f3 nn = front ? on : fk(-on.x, -on.y, -on.z);
         E = fk(fmaf(T.x, sp->emis.x, E.x), fmaf(T.y, sp->emis.y, E.y), fmaf(T.z, sp->emis.z, E.z));
@@ -1154,6 +1241,8 @@ static f3 sample_B(const sphB *s, int n, const camB *cam, int nsub, int x, int y
             float cs = cp * sth, ss = sp_ * sth;
             f3 nd = fk(fmaf(w.x, cth, fmaf(vv.x, ss, uu.x * cs)), fmaf(w.y, cth, fmaf(vv.y, ss, uu.y * cs)),
                        fmaf(w.z, cth, fmaf(vv.z, ss, uu.z * cs)));
+            if (g_bvar & PO_BV_RENORM)
+                nd = fnorm(nd);
             o = p; /* main.cpp:55 normalises u*cos*sin + v*sin*sin + w*cos, a unit vector by construction */
             d = nd;
             continue;
@@ -1212,14 +1301,20 @@ static float mean_B(uint64_t sum, int samps)
     return samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)samps) : 0.0f;
 }
 
+/* quant_B is exact on [0, 2^30]; other values (NaN, negative, larger) are
+ * clipped -- counted by po_render_xs_f32_ex (the kernel's
+ * PTG_FLAG_COUNT_NONFINITE) */
+static int in_quant_range_B(float c) { return c >= 0.0f && c <= 0x1p30f; }
+
 static f3 subpixel_B(const sphB *s, int n, const camB *cam, int samps, int nsub, int x, int y,
-                     int sx, int sy, uint64_t key, uint64_t *segs)
+                     int sx, int sy, uint64_t key, uint64_t *segs, uint64_t *bad)
 {
     uint64_t ax = 0, ay = 0, az = 0;
     for (int k = 0; k < samps; ++k) {
         int sg = 0;
         f3 c = sample_B(s, n, cam, nsub, x, y, sx, sy, po_sample_state(key, (uint32_t)k), &sg);
         *segs += (uint64_t)sg;
+        *bad += !(in_quant_range_B(c.x) && in_quant_range_B(c.y) && in_quant_range_B(c.z));
         ax += quant_B(c.x);
         ay += quant_B(c.y);
         az += quant_B(c.z);
@@ -1232,6 +1327,13 @@ static float clampf_B(float v) { return v < 0.0f ? 0.0f : (1.0f < v ? 1.0f : v);
 int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
                      uint64_t seed, int y0, int y1, int ystep, int nthreads, float *image, uint64_t *segments)
 {
+    return po_render_xs_f32_ex(s, n, cam, W, H, samps, nsub, seed, y0, y1, ystep, nthreads, image, segments, NULL);
+}
+
+int po_render_xs_f32_ex(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                        uint64_t seed, int y0, int y1, int ystep, int nthreads, float *image, uint64_t *segments,
+                        uint64_t *out_of_range)
+{
     if (check_args(n, W, H, samps, nsub) || ystep <= 0)
         return -1;
     sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
@@ -1239,9 +1341,9 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
     prep_B(s, n, cam, sb, &cb);
     cb.invW = 1.0f / (float)W;
     cb.invH = 1.0f / (float)H;
-    uint64_t total = 0;
+    uint64_t total = 0, nbad = 0;
     float q = 1.0f / (float)(nsub * nsub);
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total, nbad)
     for (int y = y0; y < y1; y += ystep) {
         for (int x = 0; x < W; ++x) {
             f3 pix = fk(0, 0, 0);
@@ -1249,9 +1351,10 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
                 for (int sx = 0; sx < nsub; ++sx) {
                     uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) +
                                   (uint64_t)(sy * nsub + sx);
-                    uint64_t segs = 0;
-                    f3 a = subpixel_B(sb, n, &cb, samps, nsub, x, y, sx, sy, po_key_hash(seed, ps), &segs);
+                    uint64_t segs = 0, bad = 0;
+                    f3 a = subpixel_B(sb, n, &cb, samps, nsub, x, y, sx, sy, po_key_hash(seed, ps), &segs, &bad);
                     total += segs;
+                    nbad += bad;
                     pix = fk(fmaf(clampf_B(a.x), q, pix.x), fmaf(clampf_B(a.y), q, pix.y),
                              fmaf(clampf_B(a.z), q, pix.z));
                 }
@@ -1264,6 +1367,8 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
     free(sb);
     if (segments)
         *segments = total;
+    if (out_of_range)
+        *out_of_range = nbad;
     return 0;
 }
 
@@ -1272,6 +1377,14 @@ void po_mode_b_math(const float *a, const float *b, size_t n, float *quot, float
     for (size_t i = 0; i < n; ++i) {
         quot[i] = div_B(a[i], b[i]);
         root[i] = sqrt_B(a[i]);
+    }
+}
+
+void po_mode_b_roots(const float *a, size_t n, float *sq_scan, float *rsq)
+{
+    for (size_t i = 0; i < n; ++i) {
+        sq_scan[i] = sqrt_scan_B(a[i]);
+        rsq[i] = rsqrt_B(a[i]);
     }
 }
 

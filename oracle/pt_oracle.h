@@ -138,11 +138,23 @@ int po_render_xs_f64(const po_sphere *s, int n, const po_camera *cam, int W, int
 int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
                      uint64_t seed, int y0, int y1, int ystep, int nthreads, float *image,
                      uint64_t *segments);
+/* ... and *out_of_range = paths with a radiance component outside [0, 2^30]
+ * (NaN, negative, huge: clipped by the exact accumulation; the kernel's
+ * PTG_FLAG_COUNT_NONFINITE counter) */
+int po_render_xs_f32_ex(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                        uint64_t seed, int y0, int y1, int ystep, int nthreads, float *image, uint64_t *segments,
+                        uint64_t *out_of_range);
 /* One Mode-B path for a given (pixel, sub, sample): returns radiance and
  * segment count -- used by the per-sample GPU parity test. */
 /* Mode B arithmetic primitives: quot[i] = div_B(a[i], b[i]) (b > 0),
  * root[i] = sqrt_B(a[i]) */
 void po_mode_b_math(const float *a, const float *b, size_t n, float *quot, float *root);
+/* the scan's square root (sqrt_scan_B) and the normalising rsqrt (rsqrt_B) of a[i] > 0 */
+void po_mode_b_roots(const float *a, size_t n, float *sq_scan, float *rsq);
+/* Mode B' (error decomposition): flags swap Mode B's approximations for
+ * accurate fp32 operations (pt_oracle.c PO_BV_*); 0 = Mode B */
+void po_set_mode_b_variant(int flags);
+int po_get_mode_b_variant(void);
 /* Mode B cos/sin(2 pi m 2^-24) of 24-bit integers m (out: n {cos, sin} pairs) */
 void po_sincos2pi(const uint32_t *m, size_t n, float *out);
 /* Mode B scene layout: anchor axis per sphere (-1: camera-facing anchor or not

@@ -70,11 +70,15 @@ def lib():
             "po_xorshift32": (U32, [P]),
             "po_render_xs_f64": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P]),
             "po_render_xs_f32": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P]),
+            "po_render_xs_f32_ex": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P, P]),
             "po_sample_f32": (I, [P, I, P, I, I, I, U64, I, I, I, I, U32, P]),
             "po_tonemap": (None, [P, C.c_size_t, P]),
             "po_scan_layout": (I, [P, I, P, P, P]),
             "po_sincos2pi": (None, [P, C.c_size_t, P]),
             "po_mode_b_math": (None, [P, P, C.c_size_t, P, P]),
+            "po_mode_b_roots": (None, [P, C.c_size_t, P, P]),
+            "po_set_mode_b_variant": (None, [I]),
+            "po_get_mode_b_variant": (I, []),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -183,6 +187,40 @@ def render_xs_f32(spheres, cam, W, H, samps, nsub=2, seed=0x5EED0001, rows=None,
     return img.reshape(H, W, 3), int(segs[0])
 
 
+# Mode B' flags (pt_oracle.c): each swaps one deliberate approximation of
+# Mode B for the accurate fp32 operation (error decomposition only)
+BV_IEEE_SQRT, BV_IEEE_DIV, BV_LIBM_TRIG, BV_RENORM, BV_FULL_SCAN, BV_LEX = 1, 2, 4, 8, 16, 32
+BV_DISC_NAIVE = 64  # round 1's discriminant hb^2 - a c for small spheres (a formulation, not an approximation)
+BV_ALL = 63  # every approximation swapped for the accurate fp32 operation
+
+
+class mode_b_variant:
+    """Context manager: render Mode B with the given B' flags (0 = Mode B)."""
+
+    def __init__(self, flags: int):
+        self.flags = flags
+
+    def __enter__(self):
+        self.prev = lib().po_get_mode_b_variant()
+        lib().po_set_mode_b_variant(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        lib().po_set_mode_b_variant(self.prev)
+
+
+def render_xs_f32_count(spheres, cam, W, H, samps, nsub=2, seed=0x5EED0001, rows=None, nthreads=8):
+    """Mode B image, segments and the count of paths whose radiance the exact
+    accumulation clips (NaN / negative / > 2^30)."""
+    y0, y1, ys = rows if rows is not None else (0, H, 1)
+    img = np.zeros((H * W * 3,), dtype=np.float32)
+    cnt = np.zeros(2, dtype=np.uint64)
+    rc = lib().po_render_xs_f32_ex(ptr(spheres), len(spheres), ptr(cam), W, H, samps, nsub, seed,
+                                   y0, y1, ys, nthreads, ptr(img), ptr(cnt[:1]), ptr(cnt[1:]))
+    assert rc == 0
+    return img.reshape(H, W, 3), int(cnt[0]), int(cnt[1])
+
+
 def sample_f32(spheres, cam, W, H, nsub, seed, x, y, sx, sy, sample):
     out = np.zeros(3, dtype=np.float32)
     segs = lib().po_sample_f32(ptr(spheres), len(spheres), ptr(cam), W, H, nsub, seed,
@@ -216,6 +254,15 @@ def sincos2pi(m):
     out = np.zeros((m.size, 2), dtype=np.float32)
     lib().po_sincos2pi(ptr(m), m.size, ptr(out))
     return out
+
+
+def mode_b_roots(a):
+    """Mode B's scan square root and normalising reciprocal square root."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    s = np.zeros_like(a)
+    r = np.zeros_like(a)
+    lib().po_mode_b_roots(ptr(a), a.size, ptr(s), ptr(r))
+    return s, r
 
 
 def mode_b_math(a, b):

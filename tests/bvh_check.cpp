@@ -70,7 +70,10 @@ static void check_layout(const std::vector<ptg_sphere> &s, const BvhBuild &b, co
 static void check_scene(const std::vector<ptg_sphere> &s)
 {
     const int n = (int)s.size();
-    BvhBuild b = build_bvh(s.data(), n, 1000.0);
+    std::vector<char> huge_flags(n);
+    for (int i = 0; i < n; ++i)
+        huge_flags[i] = s[i].radius >= 1000.0;
+    BvhBuild b = build_bvh(s.data(), n, huge_flags);
     std::vector<int> seen(n, 0);
     for (int i : b.big)
         seen[i] += 1;

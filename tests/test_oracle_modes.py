@@ -29,9 +29,11 @@ def test_modes_agree_statistically(name):
     for img in (a_xs, b_xs):
         assert abs(img.mean() - a_mt.mean()) < 0.02 * max(a_mt.mean(), 0.05) + 0.004
     # same random streams: A/xs and B follow identical paths except where fp32
-    # rounding flips a decision -> small RMSE, and segment counts within 1 %
+    # rounding flips a decision -> the north star's per-pixel RMSE < 1e-3
+    # (measured at 256 spp: box 4.8e-5, box_mirror 1.8e-4, simple 3e-8), and
+    # segment counts within 1 %
     rmse = float(np.sqrt(((a_xs - b_xs.astype(np.float64)) ** 2).mean()))
-    assert rmse < 0.02, rmse
+    assert rmse < 1e-3, rmse
     assert abs(segs_a - segs_b) / segs_a < 0.01
 
 
@@ -75,9 +77,10 @@ def test_mode_b_sincos_table_accuracy():
 
 def test_mode_b_division_and_sqrt_accuracy():
     """Mode B's deterministic division (Newton reciprocal + residual
-    correction) and square root (Goldschmidt) over 10^6 operands spanning
-    1e-8 .. 1e8: division within 2 ulp (measured 0.5), sqrt within 6e-6 relative (measured 4.7e-6); sqrt of
-    zero and negative values is 0."""
+    correction) and square root (Goldschmidt + a Newton residual step) over
+    10^6 operands spanning 1e-8 .. 1e8: division within 2 ulp (measured 0.5),
+    sqrt within 1.2e-7 relative (about 1 ulp; measured 0.63 ulp); sqrt of zero
+    and negative values is 0."""
     rng = np.random.default_rng(11)
     n = 1_000_000
     a = (10.0 ** rng.uniform(-8, 8, n) * rng.choice([-1.0, 1.0], n)).astype(np.float32)
@@ -88,7 +91,7 @@ def test_mode_b_division_and_sqrt_accuracy():
     assert (np.abs(q - exact) <= 2 * ulp).all()
     pos = a > 0
     rel = np.abs(r[pos] - np.sqrt(a[pos].astype(np.float64))) / np.sqrt(a[pos].astype(np.float64))
-    assert rel.max() < 6e-6
+    assert rel.max() < 1.2e-7
     assert (r[~pos] == 0).all()
     z, rz = po.mode_b_math(np.array([0.0, -0.0, 4.0], np.float32), np.ones(3, np.float32))
-    assert rz[0] == 0 and rz[1] == 0 and abs(rz[2] - 2.0) < 1e-5
+    assert rz[0] == 0 and rz[1] == 0 and rz[2] == 2.0
