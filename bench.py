@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
 """Benchmark: Mray-samples/s of the MI355X render loop (BASELINE.json metric).
 
-One step = one full frame of the workload (default: box_scene.hpp at
-1920x1080, 1024 spp = 256 samples per sub-pixel) rendered by the HIP
-megakernel, scene and output already resident in HBM.  With N ranks
-(torchrun, one process per GPU) the frame is tile-sharded by interleaved row
-bands and the step includes the single gather (RCCL over xGMI) to rank 0 and
-the un-shard; value = whole-frame samples / max-over-ranks time (strong
-scaling: the frame size is fixed).
+One step = one full frame of the workload rendered by the HIP megakernel,
+scene and output already resident in HBM.  Workload (--workload auto): on one
+GPU the metric's frame, box_scene.hpp at 1920x1080, 1024 spp (256 samples per
+sub-pixel); with N > 1 ranks (torchrun, one process per GPU) BASELINE.json
+configs[3] = C4, box_scene at 3840x2160, 4096 spp, tile-sharded by
+interleaved row bands, the step including the single gather (RCCL over xGMI)
+to rank 0 and the un-shard.  value = whole-frame samples / max-over-ranks time
+(strong scaling: the frame is fixed for a given N; C4 on one GPU runs at the
+same per-sample rate as the 1080p frame, 12.35 vs 12.4 G samples/s in round 1,
+so the per-N values compare).  --workload c1..c5 / bench pick one config for
+every N.
 
 Also reported:
   roofline     -- VALU fp32 roofline of the render kernel: algorithmic FLOP
@@ -38,13 +42,65 @@ METRIC = "Mray-samples/sec at 1920×1080×1024spp; per-pixel RMSE vs CPU ref"
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 
 
+# BASELINE.json configs (C1..C5) plus the metric's own frame
+WORKLOADS = {
+    "bench": ("box", 1920, 1080, 1024),       # the metric: box_scene at 1920x1080x1024spp on one MI355X
+    "c1": ("simple", 400, 300, 64),
+    "c2": ("box", 1024, 768, 256),
+    "c3": ("box_mirror", 1920, 1080, 1024),
+    "c4": ("box", 3840, 2160, 4096),          # tile-sharded over 8 GPUs
+    "c5": ("synthetic:10000", 1920, 1080, 1024),
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s, gpu_image=None, seed=None, quality_rows=4):
+def host_cpu_info():
+    """The host the CPU baseline runs on: the machine's CPU count and model,
+    the CPUs this process may run on, the cgroup CPU quota and
+    OMP_NUM_THREADS (on the GPU box the job's share of a large machine)."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            info["cgroup_cpus"] = None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return info
+
+
+def default_cpu_threads():
+    """Threads for the CPU baseline: the job's CPU share -- OMP_NUM_THREADS
+    when set (16 on the GPU box, where os.cpu_count() is the whole machine's
+    CPUs shared with other jobs), else the CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(scene_name, W, H, samps, nsub, threads, row_step, gpu_image=None, seed=None, quality_rows=4):
     """Time the repo's OpenMP CPU path (oracle Mode A: reference arithmetic,
-    double + mt19937 row seeding) on a bounded subset of the frame's rows.
+    double + mt19937 row seeding) on every row_step-th row of the frame, all
+    samples of those rows; the rate extrapolates linearly to the frame.
 
     With `gpu_image` (the benchmarked frame, [H, W, 3] float32) the same leg
     also checks quality on `quality_rows` evenly spaced rows:
@@ -64,28 +120,22 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, budget_s, gpu_image=Non
     sp = scn.to_array().view(po.SPHERE_DT)
     ca = cam.to_array().view(po.CAMERA_DT)
     img = np.zeros(W * H * 3)
-    rows = 0
+    rows = len(range(0, H, row_step))
     t0 = time.perf_counter()
-    offsets = []
-    for k in range(0, 64, 8):  # row sets y = k, k+64, k+128, ...
-        for kk in (k, k + 4):
-            n = len(range(kk, H, 64))
-            rc = po.lib().po_render_mt(po.ptr(sp), len(sp), po.ptr(ca), W, H, samps, nsub, 1, kk, H, 64, threads,
-                                       po.ptr(img))
-            assert rc == 0
-            rows += n
-            offsets.append(kk)
-            if time.perf_counter() - t0 >= budget_s:
-                break
-        if time.perf_counter() - t0 >= budget_s:
-            break
+    rc = po.lib().po_render_mt(po.ptr(sp), len(sp), po.ptr(ca), W, H, samps, nsub, 1, 0, H, row_step, threads,
+                               po.ptr(img))
+    assert rc == 0
     dt = time.perf_counter() - t0
     nsamp = rows * W * samps * nsub * nsub
-    out = {"value": round(nsamp / dt / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "port",
+    rate = nsamp / dt
+    out = {"value": round(rate / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "port",
            "seconds": round(dt, 2),
-           "sample": (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp, {rows} of {H} rows "
-                      f"(y = k mod 64 for k in {offsets}); oracle Mode A (double, mt19937 per row, "
-                      f"reference arithmetic) in an OpenMP schedule(dynamic,1) row loop")}
+           "frame_seconds_extrapolated": round(W * H * samps * nsub * nsub / rate, 1),
+           "host": host_cpu_info(),
+           "sample": (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp: every {row_step}th row ({rows} of {H}, "
+                      f"all their samples) timed, the frame extrapolated linearly; oracle Mode A (double, mt19937 "
+                      f"per row, reference arithmetic) in an OpenMP schedule(dynamic,1) row loop on {threads} "
+                      f"threads")}
     if gpu_image is not None and quality_rows > 0:
         step_y = max(1, H // quality_rows)
         ys = np.arange(step_y // 2, H, step_y)[:quality_rows]  # image-space y (main.cpp:181: y = 0 at the bottom)
@@ -128,15 +178,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="box")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=1024, help="total samples per pixel (4 sub-pixels)")
+    ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto",
+                    help="BASELINE.json config (auto: the metric's box 1920x1080x1024spp frame on one GPU, "
+                         "C4's box 3840x2160x4096spp frame when sharded over N > 1 GPUs)")
+    ap.add_argument("--scene", default=None, help="overrides the workload's scene")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None, help="total samples per pixel (4 sub-pixels)")
     ap.add_argument("--band-rows", type=int, default=ptgpu.DEFAULT_BAND_ROWS)
     ap.add_argument("--chunk", type=int, default=0, help="samples per sub-pixel per work unit (0 = auto)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = the job's CPU share: OMP_NUM_THREADS, else the affinity mask)")
+    ap.add_argument("--cpu-row-step", type=int, default=8,
+                    help="CPU baseline: time every k-th row of the frame (8 = one eighth)")
     ap.add_argument("--quality-rows", type=int, default=4,
                     help="rows checked against the CPU oracle in the cpu_baseline leg (0 = none)")
     args = ap.parse_args()
@@ -159,9 +214,12 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
+    wl = args.workload if args.workload != "auto" else ("bench" if world == 1 else "c4")
+    wscene, wW, wH, wspp = WORKLOADS[wl]
+    args.scene = args.scene or wscene
     nsub = 2  # main.cpp:202
-    W, H = args.width, args.height
-    samps = args.spp // (nsub * nsub)  # main.cpp:206
+    W, H = args.width or wW, args.height or wH
+    samps = (args.spp or wspp) // (nsub * nsub)  # main.cpp:206
     spp = samps * nsub * nsub
     scn = ptgpu.make_scene(args.scene, W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
@@ -181,9 +239,12 @@ def main():
         ctx.render_device(slab, cparams if count else params, segs if count else None, stream)
         if events is not None:
             events[1].record(stream)
-        if world > 1:
-            return ptgpu.render_sharded(params, slab, tile_renderer=lambda out, p: None)
-        return slab
+        out = slab
+        if world > 1:  # the ONE gather (RCCL) + the un-shard on rank 0
+            out = ptgpu.render_sharded(params, slab, tile_renderer=lambda out, p: None)
+        if events is not None:
+            events[2].record(stream)
+        return out
 
     # S_bar from the kernel's own segment counter (untimed)
     step(count=True)
@@ -193,7 +254,7 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -205,7 +266,17 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if args.steps else float("nan")
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs])) if args.steps else float("nan")
+    gather_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs])) if args.steps else float("nan")
+    per_rank = None
+    if world > 1:  # per-rank render and gather (+ un-shard on rank 0) times, HIP events on the launch stream
+        cdev0 = torch.device("cpu") if rehearsal else dev
+        mine = torch.tensor([kern_ms, gather_ms], dtype=torch.float64, device=cdev0)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = {"render_ms": [round(float(t[0]), 3) for t in allr],
+                    "gather_ms": [round(float(t[1]), 3) for t in allr],
+                    "note": "gather_ms: the RCCL gather (and rank 0's un-shard), incl. waiting for the slowest rank"}
 
     seg_total = seg_local
     if world > 1:
@@ -230,12 +301,13 @@ def main():
 
     if rank == 0:
         workload = f"{args.scene} {W}x{H} {spp}spp"
+        wl_name = wl if (args.scene, W, H, spp) == WORKLOADS[wl] else "custom"
         value = frame_samples * args.steps / elapsed / 1e6
         cpu = None
         if world == 1 and args.cpu_baseline == "auto":
             frame = slab.cpu().numpy().reshape(rows, W, 3)[:H]  # band_rows = 1, one shard: slab row = image row
-            cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads, args.cpu_seconds, frame,
-                               ptgpu.DEFAULT_SEED, args.quality_rows)
+            cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads or default_cpu_threads(),
+                               max(1, args.cpu_row_step), frame, ptgpu.DEFAULT_SEED, args.quality_rows)
         pmc = load_pmc(workload)
         traffic = pmc.get("hbm_bytes_per_launch")
         out = {
@@ -252,7 +324,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural scene from the reference's box_scene.hpp; counter-RNG seed 0x5EED0001)",
-            "config": {"workload": workload, "scene": args.scene, "width": W, "height": H, "spp": spp,
+            "config": {"workload": workload, "baseline_config": wl_name, "scene": args.scene, "width": W, "height": H, "spp": spp,
                        "samples_per_subpixel": samps, "num_subpixels": nsub, "spheres": n_sph,
                        "band_rows": args.band_rows, "chunk_samples": args.chunk or "auto",
                        "parallelism": (f"tile-sharded row bands x{world}" + (" (gloo rehearsal on one GPU)"
@@ -279,6 +351,8 @@ def main():
                          "profile": pmc.get("tag")},
             "cpu_baseline": cpu,
         }
+        if per_rank is not None:
+            out["per_rank"] = per_rank
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)

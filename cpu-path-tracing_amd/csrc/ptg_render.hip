@@ -1776,6 +1776,9 @@ int set_device(int device)
 
 extern "C" {
 
+// internal (csrc/ptg_multi.cpp): set the thread-local error of ptg_last_error
+int ptg_set_error_(int code, const char *msg) { return fail(code, msg ? msg : ""); }
+
 int ptg_abi_version(void) { return PTG_ABI_VERSION; }
 
 const char *ptg_last_error(void) { return g_last_error.c_str(); }

@@ -10,9 +10,10 @@
 //   spp      total samples per pixel (main.cpp:206: divided by the 4 sub-pixels), default 4
 //   scene    box_mirror (the reference binary's scene, main.cpp:25,208) | box | simple |
 //            synthetic:N | a scene file (pt/scene_file.hpp)
-//   devices  GPUs to split the image over: one thread per device renders the
-//            interleaved rows r = k mod N (ptg_render with shard_rank = k); the
-//            image is the same bit for bit for any device list
+//   devices  distinct GPUs to split the image over (ptg_render_multi): device k
+//            renders the interleaved rows r = k mod N, ONE RCCL gather collects
+//            them on the first device; the image is the same bit for bit for any
+//            device list (default: the current device, ptg_render)
 //   out      P3 (the reference's format) or P6 PPM, gamma-1/2.2 8-bit values
 //            (main.cpp:240-247, utils.cpp:11-16)
 //   --save-scene / --dump-json write the scene (scene file) / the scene and the
@@ -25,7 +26,6 @@
 #include <cstring>
 #include <fstream>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "pt/gpu_render.hpp"
@@ -178,36 +178,29 @@ int main(int argc, char *argv[])
     std::vector<pt::vec3> image(static_cast<std::size_t>(width) * height, pt::vec3{0, 0, 0});
     std::vector<int> const devs = parse_devices(devices);
     int const nd = static_cast<int>(devs.size());
-    std::vector<int> rcs(nd, PTG_OK);
     auto const t0 = std::chrono::steady_clock::now();
-    {
-        // one host thread per device: shard k of nd (interleaved single rows);
-        // each ptg_render adds only its own rows into the shared image
-        std::vector<std::thread> pool;
-        for (int k = 0; k < nd; ++k)
-            pool.emplace_back([&, k] {
-                ptg_params p{};
-                p.width = width;
-                p.height = height;
-                p.samples = samps;
-                p.num_subpixels = num_subpixels;
-                p.seed = seed;
-                p.band_rows = 1;
-                p.shard_rank = k;
-                p.shard_count = nd;
-                rcs[k] = ptg_render(reinterpret_cast<ptg_sphere const *>(some_scene.spheres.data()),
-                                    some_scene.spheres.size(), reinterpret_cast<ptg_camera const *>(&cam), &p, devs[k],
-                                    reinterpret_cast<double *>(image.data()));
-                if (rcs[k] != PTG_OK)
-                    std::fprintf(stderr, "device %d: render failed (%d): %s\n", devs[k], rcs[k], ptg_last_error());
-            });
-        for (auto &t : pool)
-            t.join();
+    int rc = PTG_OK;
+    if (nd == 1 && devs[0] < 0) {  // main.cpp:214-236 replaced by one call
+        rc = pt::gpu::render_image(some_scene, cam, image, width, height, samps, num_subpixels, seed);
+    } else {  // several GPUs of this process: shards + one RCCL gather
+        ptg_params p{};
+        p.width = width;
+        p.height = height;
+        p.samples = samps;
+        p.num_subpixels = num_subpixels;
+        p.seed = seed;
+        p.band_rows = 1;
+        p.shard_rank = 0;
+        p.shard_count = 1;
+        rc = ptg_render_multi(reinterpret_cast<ptg_sphere const *>(some_scene.spheres.data()), some_scene.spheres.size(),
+                              reinterpret_cast<ptg_camera const *>(&cam), &p, devs.data(), nd,
+                              reinterpret_cast<double *>(image.data()));
     }
     auto const t1 = std::chrono::steady_clock::now();
-    for (int rc : rcs)
-        if (rc != PTG_OK)
-            return 1;
+    if (rc != PTG_OK) {
+        std::fprintf(stderr, "render failed (%d): %s\n", rc, ptg_last_error());
+        return 1;
+    }
     double const secs = std::chrono::duration<double>(t1 - t0).count();
     std::fprintf(stderr, "Rendered %s %dx%d at %d spp on %d device(s) in %.3f s (%.1f Msamples/s incl. setup + copies)\n",
                  scene_name.c_str(), width, height, samps * num_subpixels * num_subpixels, nd, secs,

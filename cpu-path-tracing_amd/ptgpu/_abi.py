@@ -19,6 +19,7 @@ EXPORTS = (
     "ptg_context_create", "ptg_context_destroy", "ptg_shard_rows", "ptg_render_device",
     "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
     "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device", "ptg_scene_layout",
+    "ptg_render_multi",
 )
 
 
@@ -63,6 +64,7 @@ def lib():
             "ptg_accumulate_device": (I, [P, C.POINTER(Params), C.c_int32, C.c_int32, P, P]),
             "ptg_resolve_device": (I, [P, C.POINTER(Params), C.c_int32, P, P]),
             "ptg_scene_layout": (I, [P, C.c_size_t, P, P, P]),
+            "ptg_render_multi": (I, [P, C.c_size_t, P, C.POINTER(Params), C.POINTER(C.c_int), I, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

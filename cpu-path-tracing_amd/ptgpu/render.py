@@ -101,6 +101,22 @@ def render(scn, cam, image: np.ndarray, width: int, height: int, samples: int, n
     return image
 
 
+def render_multi(scn, cam, image: np.ndarray, width: int, height: int, samples: int, devices,
+                 num_subpixels: int = 2, seed: int = DEFAULT_SEED, band_rows: int = DEFAULT_BAND_ROWS) -> np.ndarray:
+    """ptg_render_multi: the drop-in render over several GPUs of this process
+    (distinct devices) -- shards rendered concurrently, ONE RCCL gather to
+    devices[0], un-shard there; the image equals render()'s bit for bit."""
+    sp = _spheres_array(scn)
+    ca = _camera_array(cam)
+    if image.dtype != np.float64 or not image.flags["C_CONTIGUOUS"] or image.size != width * height * 3:
+        raise ValueError("image must be a C-contiguous float64 array of width*height*3 values")
+    p = make_params(width, height, samples, num_subpixels, seed, band_rows)
+    devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+    check(lib().ptg_render_multi(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), C.byref(p),
+                                 devs, len(devices), image.ctypes.data_as(C.c_void_p)), "ptg_render_multi")
+    return image
+
+
 def scene_layout(scn, cam):
     """Host-side scene preparation (ptg_scene_layout, no device needed): the
     anchor axis of each huge sphere (-1: camera-facing anchor, or not huge)

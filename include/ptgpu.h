@@ -111,6 +111,17 @@ int ptg_device_count(int *count);
 int ptg_render(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam,
                const ptg_params *params, int device, double *image_rgb);
 
+/* ---- single-process multi-GPU drop-in ---------------
+ * The same contract as ptg_render (params->shard_count must be 1: the call
+ * shards the frame itself), rendered on n_devices distinct GPUs of this
+ * process: device k renders the interleaved row bands b with
+ * b % n_devices == k (band_rows from params), ONE ncclGather (RCCL over xGMI,
+ * rccl.h:745) collects the slabs on devices[0], which un-shards the frame.
+ * The image equals ptg_render's bit for bit (the RNG is keyed by the global
+ * pixel).  Replaces main.cpp:214-236 for a caller owning several GPUs. */
+int ptg_render_multi(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam,
+                     const ptg_params *params, const int *devices, int n_devices, double *image_rgb);
+
 /* ---- device-resident path (bench, multi-GPU) --------------------------
  * A context holds the prepared scene in HBM on one device. */
 int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int device,

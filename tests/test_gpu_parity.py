@@ -346,24 +346,30 @@ def test_scene_file_renders_like_the_builtin_scene(tmp_path):
 
 
 def test_cli_renders_and_splits_over_devices(tmp_path):
-    """The C++ CLI (host/main.cpp): one thread per listed device renders the
-    interleaved rows k mod N; two shards on the same GPU give the same P6
-    bytes as one, and those are the reference's color_to_int of the drop-in
-    image (utils.cpp:11-16)."""
+    """The C++ CLI (host/main.cpp): by default the drop-in ptg_render; with
+    --devices the single-process multi-GPU path ptg_render_multi (shards +
+    ONE RCCL gather) -- on this one-GPU box a one-rank communicator, whose
+    P6 bytes equal the default's; a repeated device is refused (RCCL needs
+    one rank per GPU).  The bytes are the reference's color_to_int of the
+    drop-in image (utils.cpp:11-16)."""
     _require_gpu()
     import os
     import subprocess
     cli = os.path.join(os.path.dirname(ptgpu.LIB_PATH), "pt_render_gpu")
     W, H, spp = 40, 30, 16
     outs = {}
-    for devs in ("0", "0,0"):
-        out = tmp_path / f"img_{devs.replace(',', '_')}.ppm"
-        r = subprocess.run([cli, "--scene", "box", "--width", str(W), "--height", str(H), "--spp", str(spp),
-                            "--devices", devs, "--format", "p6", "--out", str(out)],
-                           capture_output=True, text=True, timeout=120)
+    for devs in (None, "0"):
+        out = tmp_path / f"img_{devs}.ppm"
+        cmd = [cli, "--scene", "box", "--width", str(W), "--height", str(H), "--spp", str(spp), "--format", "p6",
+               "--out", str(out)] + (["--devices", devs] if devs else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         outs[devs] = out.read_bytes()
-    assert outs["0"] == outs["0,0"]
+    assert outs[None] == outs["0"]
+    r = subprocess.run([cli, "--scene", "box", "--width", str(W), "--height", str(H), "--devices", "0,0",
+                        "--out", str(tmp_path / "dup.ppm")], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "distinct devices" in r.stderr
+    outs["0"] = outs[None]
     header = f"P6\n{W} {H}\n255\n".encode()
     assert outs["0"].startswith(header)
     scn = ptgpu.box_scene(W, H)
@@ -435,3 +441,51 @@ def test_bvh_two_level_units_are_exact():
     for y in (0, H - 1):  # y = 0: the last slab row (tail level); H - 1: the first (head level)
         ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
         _check_equal(two[H - 1 - y], ref[H - 1 - y])
+
+
+def test_render_multi_rccl_one_rank_is_exact():
+    """ptg_render_multi (ncclCommInitAll + ONE ncclGather +
+    un-shard) executes on hardware here as a one-rank communicator: the
+    image equals the drop-in ptg_render's bit for bit for several band
+    heights; repeated devices are refused."""
+    _require_gpu()
+    W, H, samps = 52, 30, 8
+    scn = ptgpu.box_mirror_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    ref = np.zeros((H * W, 3))
+    ptgpu.render(scn, cam, ref, W, H, samps)
+    for br in (1, 4):
+        img = np.zeros((H * W, 3))
+        ptgpu.render_multi(scn, cam, img, W, H, samps, [0], band_rows=br)
+        assert np.array_equal(img, ref), br
+    with pytest.raises(ptgpu.PtgError, match="distinct devices"):
+        ptgpu.render_multi(scn, cam, np.zeros((H * W, 3)), W, H, samps, [0, 0])
+
+
+def test_render_sharded_on_nccl_backend():
+    """render_sharded (the multi-process path) on the nccl backend -- RCCL --
+    at world size 1: the gathered, un-sharded image equals the one-GPU
+    frame bit for bit (the 8-GPU run is the driver's)."""
+    _require_gpu()
+    import socket
+
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    W, H, samps = 48, 32, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    full, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        p = ptgpu.make_params(W, H, samps, 2, SEED, 1, 0, 1)
+        slab = torch.zeros(ptgpu.shard_rows(H, 1, 1) * W * 3, dtype=torch.float32, device="cuda")
+        with ptgpu.Context(scn, cam) as ctx:
+            image = ptgpu.render_sharded(p, slab, ctx=ctx)
+            torch.cuda.synchronize()
+        assert np.array_equal(image.cpu().numpy(), full)
+    finally:
+        dist.destroy_process_group()
