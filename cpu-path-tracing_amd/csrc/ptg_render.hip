@@ -114,6 +114,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // faster than with their samples split into ~96k units)
 #define PTG_TAIL_MIN_HALF_ROUNDS 3
 #endif
+#ifndef PTG_COOP_TAIL
+#define PTG_COOP_TAIL 1  // split-tail level with one chunk per wave of a workgroup: reduced in LDS (no HBM atomics)
+#endif
 #ifndef PTG_BVH_OCTANTS
 #define PTG_BVH_OCTANTS 1  // BVH: one depth-first layout per ray-direction octant (near child first)
 #endif
@@ -228,6 +231,13 @@ struct KArgs {
     // resolve_row0).  lvl_group[n_levels] = n_groups.
     int n_levels;
     int lvl_group[kMaxLevels + 1], lvl_chunk[kMaxLevels];
+    // cooperative level (linear kernel's split tail with as many chunks as a
+    // workgroup has waves): the waves of one workgroup take the chunks of one
+    // pixel group, the last wave to finish adds the others' LDS sums and
+    // resolves -- no HBM accumulator (lvl_unit[l] is a multiple of the
+    // waves per workgroup)
+    int lvl_coop[kMaxLevels];
+    int needs_resolve;  // some level accumulates in HBM: resolve_kernel from resolve_row0
     long long lvl_unit[kMaxLevels + 1];
     int resolve_row0;
     int sample_begin, sample_end;  // samples [begin, end) of every sub-pixel in this launch
@@ -876,7 +886,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         recs = lds_lin;
     }
     __shared__ float4 lds_cam[4];
+    __shared__ int lds_coop_done;  // cooperative levels: waves of the workgroup finished
     if (threadIdx.x == 0) {
+        lds_coop_done = 0;
         const CamC c = cam_of(A);
         lds_cam[0] = c.p;
         lds_cam[1] = c.b;
@@ -899,9 +911,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         ++lv;
     const long long t = unit - A.lvl_unit[lv];
     const int nlg = A.lvl_group[lv + 1] - A.lvl_group[lv];
-    const int group = A.lvl_group[lv] + (int)(t % nlg);
+    const bool coop = A.lvl_coop[lv] != 0;  // wave wv of the workgroup takes chunk wv of one pixel group
+    const int group = A.lvl_group[lv] + (int)(coop ? t / kWaves : t % nlg);
     const int len = A.lvl_chunk[lv];
-    const int s0 = A.sample_begin + (int)(t / nlg) * len;
+    const int s0 = A.sample_begin + (int)(coop ? t % kWaves : t / nlg) * len;
+    if (s0 >= A.sample_end)
+        return;  // whole wave: alignment padding before a cooperative level
     // the unit holds every sample of its pixels: resolve in the wave
     const bool in_wave = lv == 0 && A.single_chunk;
     const int slab_row = group / A.waves_per_row;
@@ -1169,17 +1184,36 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (in_wave) {
-        // the unit holds every sample of its pixels: resolve in the wave
-        // (main.cpp:195-196, same arithmetic as resolve_kernel) and write
-        // 12 B per pixel -- the only HBM traffic of the frame
+    bool coop_last = false;
+    if (coop) {
+        // publish this wave's sums (its LDS adds are complete), count it; the
+        // wave that completes the count adds every wave's sums and resolves
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        int prev = 0;
+        if (lane == 0)
+            prev = __hip_atomic_fetch_add(&lds_coop_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prev = __shfl(prev, 0, 64);
+        coop_last = prev == kWaves - 1;
+        if (!coop_last)
+            return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (in_wave || coop_last) {
+        // the unit (or the workgroup) holds every sample of its pixels:
+        // resolve here (main.cpp:195-196, same arithmetic as resolve_kernel)
+        // and write 12 B per pixel -- the only HBM traffic of the frame
         if (lane < npix && r < A.H) {
             f3 pix = mk3(0.0f, 0.0f, 0.0f);
             for (int j = 0; j < A.lanes_per_pixel; ++j) {
                 const int sl = lane * A.lanes_per_pixel + j;
                 float m[3];
                 for (int c = 0; c < 3; ++c) {
-                    const unsigned long long sum = lds_acc[wv][sl + 64 * c];
+                    unsigned long long sum = lds_acc[wv][sl + 64 * c];
+                    if (coop_last) {
+                        sum = 0ull;
+                        for (int w = 0; w < kWaves; ++w)  // exact: integer sums in any order
+                            sum += lds_acc[w][sl + 64 * c];
+                    }
                     const float mean = A.samps > 0 ? (float)(((double)sum * 0x1p-32) / (double)A.samps) : 0.0f;
                     m[c] = mean < 0.0f ? 0.0f : (1.0f < mean ? 1.0f : mean);
                 }
@@ -1690,7 +1724,10 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.lvl_chunk[0] = chunk;
     A.lvl_unit[0] = 0;
     A.lvl_unit[1] = A.n_units;
+    for (int l = 0; l < kMaxLevels; ++l)
+        A.lvl_coop[l] = 0;
     A.resolve_row0 = 0;
+    A.needs_resolve = !A.single_chunk;
     // Split tail: with whole-pixel units, the grid ends when its slowest last
     // units end (a unit is ~1/16 of the frame per wave slot here).  The last
     // rows -- about one round of the device's wave slots -- run instead as
@@ -1705,15 +1742,24 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
         const bool many = groups >= 5LL * ctx->wave_slots;
         // level row counts: halves of what is left, the last level takes the rest
         int rows_left = tail_rows, row = A.slab_rows - tail_rows;
-        A.resolve_row0 = row;
+        A.resolve_row0 = A.slab_rows;  // no accumulating level yet
         A.lvl_group[1] = row * A.waves_per_row;
         A.lvl_unit[1] = A.lvl_group[1];  // head: one unit per group
         int l = 1;
+        constexpr int kLinWaves = kBlock / 64;
         for (; l <= PTG_TAIL_LEVELS && rows_left > 0; ++l) {
             const int rows = l == PTG_TAIL_LEVELS ? rows_left : (rows_left + 1) / 2;
             const int tc = (many ? PTG_TAIL_CHUNKS_MANY : PTG_TAIL_CHUNKS) << (l - 1);
             const int ch = (nsamp + tc - 1) / tc;
             const int nch = (nsamp + ch - 1) / ch;
+            // one chunk per wave of a (linear-kernel) workgroup: the level's
+            // sums stay in LDS; its first unit starts a workgroup
+            const bool coop = PTG_COOP_TAIL && ctx->n <= kLinearMax && nch == kLinWaves;
+            if (coop)
+                A.lvl_unit[l] = (A.lvl_unit[l] + kLinWaves - 1) / kLinWaves * kLinWaves;
+            else if (A.resolve_row0 == A.slab_rows)
+                A.resolve_row0 = row;
+            A.lvl_coop[l] = coop ? 1 : 0;
             row += rows;
             rows_left -= rows;
             A.lvl_chunk[l] = ch;
@@ -1722,6 +1768,9 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
         }
         A.n_levels = l;
         A.n_units = A.lvl_unit[l];
+        A.needs_resolve = A.resolve_row0 < A.slab_rows;
+        if (!A.needs_resolve)
+            A.resolve_row0 = 0;
     }
 #if PTG_BVH_HEAD_CHUNK > 0
     // BVH frames/shards below their split-tail threshold (e.g. 8-way shards
@@ -1747,6 +1796,7 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
             A.lvl_unit[2] = A.lvl_unit[1] + (long long)(groups - A.lvl_group[1]) * tn;
             A.n_levels = 2;
             A.n_units = A.lvl_unit[2];
+            A.needs_resolve = 1;
         }
     }
 #endif
@@ -2075,8 +2125,8 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     int grid = 0;
     if ((rc = fill_launch(ctx, params, A, grid)))
         return rc;
-    // several units per pixel, a split tail, or no samples at all
-    const bool resolve = !A.single_chunk || A.n_levels > 1 || grid == 0;
+    // several units per pixel, a split tail accumulated in HBM, or no samples at all
+    const bool resolve = A.needs_resolve || grid == 0;
     if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
         return rc;
     A.out = d_slab;
