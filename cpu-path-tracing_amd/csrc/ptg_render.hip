@@ -145,6 +145,21 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
                           // (measured with octant layouts + SAH: 6 beats 4 by 7 %, 5 and 7 by 1-2 %)
 #endif
+#ifndef PTG_BLOCK_STATS
+#define PTG_BLOCK_STATS 0  // debug builds only: wave-level execution counts of the linear kernel's blocks (ptg_dbg_stats)
+#endif
+#if PTG_BLOCK_STATS
+// [0] main-loop iterations, [1] scans, [2] small-sphere root parts, [3] extra box-mode walls,
+// [4] diffuse/dielectric blocks, [5] mirror blocks, [6] refill batches, [7] small-sphere pre-tests
+__device__ unsigned long long ptg_dbg_stats[256 * 16];
+#define PTG_STAT(i)                                                                                    \
+    do {                                                                                               \
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                                        \
+            atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + (i)], 1ull);                            \
+    } while (0)
+#else
+#define PTG_STAT(i) ((void)0)
+#endif
 #ifndef PTG_WAVE_STATS
 #define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
 #endif
@@ -373,8 +388,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // a small sphere no lane's ray line meets cannot win: the wave skips
         // the root (exact: "win" below requires disc >= 0)
         if constexpr (kKind == kSmall) {
+            PTG_STAT(7);
             if (__ballot(!(disc < 0.0f)) == 0ull)
                 return;
+            PTG_STAT(2);
         }
 #endif
         // disc < 0 is rejected below whatever sq is: no clamp
@@ -462,12 +479,14 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         const float bqm = bq * kPlaneMargin;
         bool need[3];
         for (int k = 0; k < 3; ++k) {
-            // a missing wall is never needed (u = inf; also guarded by the
-            // uniform per-axis record flags)
-            const bool has = comp(d, k) >= 0.0f ? A.rec_plus[k] >= 0 : A.rec_minus[k] >= 0;
-            need[k] = (k != kn) & has & !(bn * v[k] < u[k] * bqm);
+            // a missing wall is never needed: its u is +inf, so bn v < u bqm
+            // holds for any v (also guarded explicitly by u < inf -- a test of
+            // values: selecting the kernel-argument record offsets per lane
+            // compiled to three dependent global loads)
+            need[k] = (k != kn) & (u[k] < HUGE_VALF) & !(bn * v[k] < u[k] * bqm);
         }
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
+            PTG_STAT(3);
             if (!in_room) {
                 for (; i < A.end_ax[0]; ++i)
                     test(i, std::integral_constant<int, kAxX>{});
@@ -766,6 +785,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     if (__ballot(isD | isG) != 0ull)
 #endif
     {
+        PTG_STAT(4);
         float cp = 0.0f, sp = 0.0f, ra = 0.0f;
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
             const uint32_t m_phi = draw_bits(st);
@@ -810,6 +830,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         }
     }
     if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
+        PTG_STAT(5);
         float k = dot3(on, d);
         k = k + k;
         (void)draw(st);
@@ -1056,6 +1077,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             const unsigned long long need = __ballot(!has_pre);
             const int nn = (int)__popcll(need);
             if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
+                PTG_STAT(6);
                 const bool idle = waiting || item < 0;
                 if (parked)
                     flush_parked();
@@ -1087,7 +1109,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         for (;;) {
             if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
                 break;
+            PTG_STAT(0);
             if (item >= 0) {
+                PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
                 if (segment<kBvh, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
@@ -1830,6 +1854,24 @@ extern "C" {
 int ptg_set_error_(int code, const char *msg) { return fail(code, msg ? msg : ""); }
 
 int ptg_abi_version(void) { return PTG_ABI_VERSION; }
+
+#if PTG_BLOCK_STATS
+// debug builds only: the 16 block counters summed over their 256 slots (then zeroed)
+int ptg_debug_stats_(unsigned long long *out16)
+{
+    std::vector<unsigned long long> h(256 * 16);
+    PTG_HIP(hipDeviceSynchronize());
+    PTG_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(ptg_dbg_stats), h.size() * sizeof(h[0])));
+    for (int i = 0; i < 16; ++i) {
+        out16[i] = 0;
+        for (int b = 0; b < 256; ++b)
+            out16[i] += h[b * 16 + i];
+    }
+    std::vector<unsigned long long> z(h.size(), 0ull);
+    PTG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ptg_dbg_stats), z.data(), z.size() * sizeof(z[0])));
+    return PTG_OK;
+}
+#endif
 
 const char *ptg_last_error(void) { return g_last_error.c_str(); }
 
