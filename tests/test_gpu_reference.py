@@ -52,8 +52,9 @@ def _render(scn, cam, W, H, samps, flags=0, counters=None):
 
 
 # config, scene, W, H, samples per sub-pixel, row step, regression guard
-# (measured RMSE vs Mode A/xs on these rows: C1 5.8e-5, C2 3.0e-4, C3 5.0e-5)
-CONFIGS = [("C1", "simple", 400, 300, 16, 1, 2e-4),
+# (measured RMSE vs Mode A/xs on these rows: C1 5.8e-5 - 1.8e-4 (single diverging paths of the
+# 30-emission light move it by ~1e-4 each), C2 3.0e-4, C3 5.0e-5)
+CONFIGS = [("C1", "simple", 400, 300, 16, 1, 5e-4),
            ("C2", "box", 1024, 768, 64, 16, 9e-4),
            ("C3", "box_mirror", 1920, 1080, 256, 67, 3e-4)]
 

@@ -39,6 +39,10 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--f64", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--row-step", type=int, default=1, help="compare every k-th row only (C5: the double oracle scans 10,000 spheres)")
+    ap.add_argument("--chunk", type=int, default=32, help="oracle rows per call (progress lines in between)")
+    ap.add_argument("--skip-mode-b", action="store_true",
+                    help="no Mode B comparison (C5: its linear fp32 scan of 10,000 spheres is ~5x slower than Mode A's)")
     a = ap.parse_args()
     W, H, nsub = a.width, a.height, 2
     samps = a.spp // (nsub * nsub)
@@ -58,26 +62,38 @@ def main():
 
     sp = scn.to_array().view(po.SPHERE_DT)
     ca = cam.to_array().view(po.CAMERA_DT)
-    t0 = time.perf_counter()
-    b, _ = po.render_xs_f32(sp, ca, W, H, samps, nsub, seed, nthreads=a.threads)
-    t_b = time.perf_counter() - t0
-    b = b.astype(np.float64)
-    print(f"oracle Mode B frame done ({t_b:.1f} s)", file=sys.stderr, flush=True)
+    ys = np.arange(0, H, a.row_step)  # image-space y (main.cpp:181: y = 0 is the bottom row)
+
+    def oracle(fn, label):
+        img = np.zeros((H, W, 3), dtype=np.float64)
+        t0 = time.perf_counter()
+        for i in range(0, len(ys), a.chunk):
+            part = ys[i:i + a.chunk]
+            y0, y1 = int(part[0]), int(part[-1]) + 1
+            x, _ = fn(sp, ca, W, H, samps, nsub, seed, rows=(y0, y1, a.row_step), nthreads=a.threads)
+            img[H - 1 - part] = x[H - 1 - part]
+            print(f"{label}: {i + len(part)}/{len(ys)} rows ({time.perf_counter() - t0:.0f} s)", file=sys.stderr,
+                  flush=True)
+        return img[H - 1 - ys], time.perf_counter() - t0
+
+    gpu = gpu[H - 1 - ys]
     res = {
         "workload": f"{a.scene} {W}x{H} {samps * nsub * nsub}spp",
-        "pixels": W * H,
+        "rows_compared": f"{len(ys)} of {H}" + (f" (every {a.row_step}th)" if a.row_step > 1 else ""),
+        "pixels": int(len(ys) * W),
         "gpu_seconds_incl_setup": round(t_gpu, 3),
-        "oracle_mode_b_seconds": round(t_b, 1),
         "oracle_threads": a.threads,
-        "max_abs_vs_mode_b": float(np.abs(gpu - b).max()),
-        "rmse_vs_mode_b": float(np.sqrt(((gpu - b) ** 2).mean())),
-        "pixels_differing_from_mode_b": int((np.abs(gpu - b).max(axis=2) > 0).sum()),
         "image_mean": float(gpu.mean()),
     }
+    if not a.skip_mode_b:
+        b, t_b = oracle(po.render_xs_f32, "oracle Mode B")
+        res.update({"oracle_mode_b_seconds": round(t_b, 1),
+                    "max_abs_vs_mode_b": float(np.abs(gpu - b).max()),
+                    "rmse_vs_mode_b": float(np.sqrt(((gpu - b) ** 2).mean())),
+                    "pixels_differing_from_mode_b": int((np.abs(gpu - b).max(axis=2) > 0).sum())})
     if a.f64:
-        t0 = time.perf_counter()
-        x, _ = po.render_xs_f64(sp, ca, W, H, samps, nsub, seed, nthreads=a.threads)
-        res["oracle_mode_a_xs_seconds"] = round(time.perf_counter() - t0, 1)
+        x, t_x = oracle(po.render_xs_f64, "oracle Mode A/xs")
+        res["oracle_mode_a_xs_seconds"] = round(t_x, 1)
         res["rmse_vs_mode_a_xs_f64"] = float(np.sqrt(((gpu - x) ** 2).mean()))
         res["max_abs_vs_mode_a_xs_f64"] = float(np.abs(gpu - x).max())
         res["rmse_tolerance"] = 1e-3
@@ -86,7 +102,7 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             f.write(line + "\n")
-    if res["max_abs_vs_mode_b"] != 0.0:
+    if res.get("max_abs_vs_mode_b", 0.0) != 0.0:
         sys.exit(1)
 
 
