@@ -30,6 +30,7 @@
 #include "../../include/ptgpu.h"
 #include "bvh_build.hpp"
 #include "pt_device.hpp"
+#include "ref64.hpp"
 
 using namespace ptg;
 
@@ -1362,6 +1363,8 @@ struct ptg_context {
     size_t acc_elems;
     bool acc_dirty;  // progressive sums may be in d_acc (accumulate / keep_acc resolve since the last reset)
     KArgs base;  // camera + scene fields filled
+    ptg_sphere *d_sph64;  // the scene as given (PTG_FLAG_REFERENCE_F64)
+    ptg_camera cam64;
 };
 
 namespace {
@@ -1956,6 +1959,14 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         }
         PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_trig, tab, sizeof(tab), hipMemcpyHostToDevice));
     }
+    ctx->cam64 = *cam;
+    if (n_spheres) {
+        if (hipMalloc(&ctx->d_sph64, n_spheres * sizeof(ptg_sphere)) != hipSuccess) {
+            ptg_context_destroy(ctx);
+            return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the scene (f64) failed");
+        }
+        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_sph64, spheres, n_spheres * sizeof(ptg_sphere), hipMemcpyHostToDevice));
+    }
     KArgs &A = ctx->base;
     std::memset(&A, 0, sizeof(A));
     A.trig = ctx->d_trig;
@@ -2096,6 +2107,8 @@ int ptg_context_destroy(ptg_context *ctx)
         (void)hipFree(ctx->d_bvh);
     if (ctx->d_acc)
         (void)hipFree(ctx->d_acc);
+    if (ctx->d_sph64)
+        (void)hipFree(ctx->d_sph64);
     delete ctx;
     return PTG_OK;
 }
@@ -2140,6 +2153,40 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     return PTG_OK;
 }
 
+// PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (ref64.hpp), one
+// lane per sub-pixel; out64 or out32 receives the slab
+int launch_ref64(const ptg_context *ctx, const KArgs &A, double *out64, float *out32,
+                 unsigned long long *d_segments, hipStream_t s)
+{
+    ref64::Args R{};
+    R.spheres = ctx->d_sph64;
+    R.n = ctx->n;
+    R.cam = ctx->cam64;
+    R.W = A.W;
+    R.H = A.H;
+    R.samps = A.samps;
+    R.nsub = A.nsub;
+    R.lanes_per_pixel = A.lanes_per_pixel;
+    R.pixels_per_wave = A.pixels_per_wave;
+    R.waves_per_row = A.waves_per_row;
+    R.slab_rows = A.slab_rows;
+    R.band_rows = A.band_rows;
+    R.shard_rank = A.shard_rank;
+    R.shard_count = A.shard_count;
+    R.seed = A.seed;
+    R.out64 = out64;
+    R.out32 = out32;
+    R.segments = d_segments;
+    const long long waves = (long long)A.slab_rows * A.waves_per_row;
+    const long long blocks = (waves + 3) / 4;
+    if (blocks > 0x7FFFFFFFLL)
+        return fail(PTG_ERR_UNSUPPORTED, "image too large for the reference-arithmetic mode");
+    if (blocks > 0)
+        ref64::render_kernel<<<(unsigned)blocks, 256, 0, s>>>(R);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
 int launch_resolve(const KArgs &A, hipStream_t s)
 {
     long long pixels = (long long)(A.slab_rows - A.resolve_row0) * A.W;
@@ -2167,6 +2214,8 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     int grid = 0;
     if ((rc = fill_launch(ctx, params, A, grid)))
         return rc;
+    if (params->flags & PTG_FLAG_REFERENCE_F64)
+        return launch_ref64(ctx, A, nullptr, d_slab, d_segments, reinterpret_cast<hipStream_t>(stream));
     // several units per pixel, a split tail accumulated in HBM, or no samples at all
     const bool resolve = A.needs_resolve || grid == 0;
     if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
@@ -2196,6 +2245,9 @@ int ptg_accumulate_device(ptg_context *ctx, const ptg_params *params, int32_t sa
         return rc;
     if (sample_begin < 0 || sample_end < sample_begin || sample_end > params->samples)
         return fail(PTG_ERR_INVALID_ARGUMENT, "sample range must satisfy 0 <= begin <= end <= samples");
+    if (params->flags & PTG_FLAG_REFERENCE_F64)
+        return fail(PTG_ERR_UNSUPPORTED, "progressive passes are fp32 only (the reference-arithmetic mode sums "
+                                         "its samples sequentially, main.cpp:192)");
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
@@ -2263,6 +2315,8 @@ int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const i
         return rc;
     if (n == 0)
         return PTG_OK;
+    if (params->flags & PTG_FLAG_REFERENCE_F64)
+        return fail(PTG_ERR_UNSUPPORTED, "trace_samples probes the fp32 kernel");
     PTG_HIP(hipSetDevice(ctx->device));
     KArgs A;
     int grid = 0;
@@ -2322,18 +2376,29 @@ int ptg_render(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *ca
     int32_t slab_rows = 0;
     ptg_shard_rows(params->height, params->band_rows, params->shard_count, &slab_rows);
     size_t slab_elems = (size_t)slab_rows * params->width * 3;
-    float *d_slab = nullptr;
-    std::vector<float> host(slab_elems);
+    // the reference-arithmetic mode keeps its doubles to the host image
+    const bool f64 = (params->flags & PTG_FLAG_REFERENCE_F64) != 0;
+    const size_t esz = f64 ? sizeof(double) : sizeof(float);
+    void *d_slab = nullptr;
+    std::vector<unsigned char> host(slab_elems * esz);
     rc = PTG_OK;
-    if (hipMalloc(&d_slab, slab_elems * sizeof(float)) != hipSuccess) {
+    if (hipMalloc(&d_slab, slab_elems * esz) != hipSuccess) {
         ptg_context_destroy(ctx);
         return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the image slab failed");
     }
-    rc = ptg_render_device(ctx, params, d_slab, nullptr, nullptr);
+    if (f64) {
+        KArgs A;
+        int grid = 0;
+        rc = fill_launch(ctx, params, A, grid);
+        if (rc == PTG_OK)
+            rc = launch_ref64(ctx, A, static_cast<double *>(d_slab), nullptr, nullptr, nullptr);
+    } else {
+        rc = ptg_render_device(ctx, params, static_cast<float *>(d_slab), nullptr, nullptr);
+    }
     if (rc == PTG_OK) {
         hipError_t e = hipDeviceSynchronize();
         if (e == hipSuccess)
-            e = hipMemcpy(host.data(), d_slab, slab_elems * sizeof(float), hipMemcpyDeviceToHost);
+            e = hipMemcpy(host.data(), d_slab, slab_elems * esz, hipMemcpyDeviceToHost);
         if (e != hipSuccess)
             rc = fail(PTG_ERR_HIP, std::string("render: ") + hipGetErrorString(e));
     }
@@ -2347,10 +2412,11 @@ int ptg_render(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *ca
         int r = (band * params->shard_count + params->shard_rank) * BR + (j - band * BR);
         if (r >= H)
             continue;
-        const float *src = host.data() + (size_t)j * W * 3;
         double *dst = image_rgb + (size_t)r * W * 3;
-        for (int i = 0; i < W * 3; ++i)
-            dst[i] = dst[i] + (double)src[i];  // main.cpp:196: image[row] += ...
+        const size_t off = (size_t)j * W * 3;
+        for (int i = 0; i < W * 3; ++i)  // main.cpp:196: image[row] += ...
+            dst[i] = dst[i] + (f64 ? reinterpret_cast<const double *>(host.data())[off + i]
+                                   : (double)reinterpret_cast<const float *>(host.data())[off + i]);
     }
     return PTG_OK;
 }

@@ -46,6 +46,7 @@ def _camera_array(cam) -> np.ndarray:
 
 FLAG_COUNT_TESTS = 1  # include/ptgpu.h PTG_FLAG_COUNT_TESTS
 FLAG_COUNT_NONFINITE = 2  # include/ptgpu.h PTG_FLAG_COUNT_NONFINITE (4 counters)
+FLAG_REFERENCE_F64 = 4  # include/ptgpu.h PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode)
 
 
 def _n_counters(flags: int) -> int:
@@ -86,7 +87,7 @@ def unshard_host(gathered: np.ndarray, width: int, height: int, band_rows: int, 
 
 
 def render(scn, cam, image: np.ndarray, width: int, height: int, samples: int, num_subpixels: int = 2,
-           seed: int = DEFAULT_SEED, device: int = -1) -> np.ndarray:
+           seed: int = DEFAULT_SEED, device: int = -1, flags: int = 0) -> np.ndarray:
     """Drop-in for main.cpp:214-236: image (W*H RGB doubles, reference row
     order, zero-initialised by the caller like main.cpp:210-212) receives
     += sum_sub clamp(mean radiance) / num_subpixels^2 for every pixel."""
@@ -95,7 +96,7 @@ def render(scn, cam, image: np.ndarray, width: int, height: int, samples: int, n
     img = image if image.dtype == np.float64 and image.flags["C_CONTIGUOUS"] else None
     if img is None or img.size != width * height * 3:
         raise ValueError("image must be a C-contiguous float64 array of width*height*3 values")
-    p = make_params(width, height, samples, num_subpixels, seed)
+    p = make_params(width, height, samples, num_subpixels, seed, flags=flags)
     check(lib().ptg_render(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), C.byref(p),
                            int(device), img.ctypes.data_as(C.c_void_p)), "ptg_render")
     return image

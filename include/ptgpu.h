@@ -94,6 +94,15 @@ typedef struct ptg_params {
  * negative or above 2^30 -- values the exact accumulation would clip (NaN and
  * negative to 0).  None are expected: the -m gpu tests assert 0. */
 #define PTG_FLAG_COUNT_NONFINITE 2
+/* PTG_FLAG_REFERENCE_F64: render with the reference's own double-precision
+ * arithmetic, operation for operation (src/main.cpp:30-197 and the pt
+ * library: linear strict-< scan, (-hb -+ sq)/a roots, libm-style
+ * sin/cos/pow, sequential r += c/samps) instead of the fp32 megakernel --
+ * a parity mode (csrc/ref64.hpp), several times slower.  Only the counter-RNG
+ * draws differ from the reference (as in every mode).  ptg_render keeps the
+ * doubles; ptg_render_device rounds them into its float slab.  Not for
+ * progressive passes or trace_samples (PTG_ERR_UNSUPPORTED). */
+#define PTG_FLAG_REFERENCE_F64 4
 
 typedef struct ptg_context ptg_context;
 
