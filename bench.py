@@ -192,6 +192,8 @@ def main():
                     help="CPU baseline threads (0 = the job's CPU share: OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--cpu-row-step", type=int, default=8,
                     help="CPU baseline: time every k-th row of the frame (8 = one eighth)")
+    ap.add_argument("--reference-f64", action="store_true",
+                    help="PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode, not the metric)")
     ap.add_argument("--quality-rows", type=int, default=4,
                     help="rows checked against the CPU oracle in the cpu_baseline leg (0 = none)")
     args = ap.parse_args()
@@ -224,9 +226,11 @@ def main():
     scn = ptgpu.make_scene(args.scene, W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     ctx = ptgpu.Context(scn, cam, device=local)
-    params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk)
+    f64 = ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0
+    params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
+                               flags=f64)
     cparams = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
-                                flags=ptgpu.FLAG_COUNT_TESTS)
+                                flags=ptgpu.FLAG_COUNT_TESTS | f64)
     rows = ptgpu.shard_rows(H, args.band_rows, world)
     slab = torch.zeros(rows * W * 3, dtype=torch.float32, device=dev)
     my_rows = int((ptgpu.slab_to_image_rows(H, args.band_rows, rank, world) >= 0).sum())
@@ -250,6 +254,8 @@ def main():
     step(count=True)
     torch.cuda.synchronize()
     seg_local, sph_local, box_local = (int(v) for v in segs.cpu().tolist())
+    if f64:  # the reference's linear scan: every sphere per segment (ref64.hpp counts segments only)
+        sph_local = seg_local * ctx.n_spheres
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
@@ -322,7 +328,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f64 (reference-arithmetic mode)" if f64 else "f32",
             "data": "synthetic (procedural scene from the reference's box_scene.hpp; counter-RNG seed 0x5EED0001)",
             "config": {"workload": workload, "baseline_config": wl_name, "scene": args.scene, "width": W, "height": H, "spp": spp,
                        "samples_per_subpixel": samps, "num_subpixels": nsub, "spheres": n_sph,

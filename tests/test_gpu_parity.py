@@ -489,3 +489,44 @@ def test_render_sharded_on_nccl_backend():
         assert np.array_equal(image.cpu().numpy(), full)
     finally:
         dist.destroy_process_group()
+
+
+def test_c4_frame_size_shards_are_exact():
+    """C4's frame size (box 3840x2160, BASELINE configs[3], at 8 spp here):
+    the 1-GPU frame, its 8-way interleaved shards gathered and un-sharded on
+    the device, and oracle rows (head and split-tail rows) agree bit for
+    bit."""
+    _require_gpu()
+    W, H, samps = 3840, 2160, 2
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    full, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    count = 8
+    rows = ptgpu.shard_rows(H, 1, count)
+    gathered = torch.zeros((count, rows * W * 3), dtype=torch.float32, device="cuda")
+    with ptgpu.Context(scn, cam) as ctx:
+        for k in range(count):
+            ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count))
+        image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ptgpu.unshard_device(gathered, image, W, H, 1, count)
+        torch.cuda.synchronize()
+    assert np.array_equal(image.cpu().numpy(), full)
+    sp, ca = _oracle_scene(scn, cam)
+    for y in (0, 1, 1337, H - 1):
+        ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1))
+        _check_equal(full[H - 1 - y], ref[H - 1 - y])
+
+
+def test_c5_frame_size_rows_are_exact():
+    """C5's frame size (synthetic:10000 at 1920x1080, BVH kernel with
+    whole-pixel units and a split tail, at 64 spp here): rows of the head
+    and of the tail equal the oracle's linear scan bit for bit."""
+    _require_gpu()
+    W, H, samps = 1920, 1080, 16
+    scn = ptgpu.make_scene("synthetic:10000", W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    full, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    sp, ca = _oracle_scene(scn, cam)
+    for y in (0, 300):  # y = 0: the last slab row (split tail); 300: a head row in the sphere field
+        ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1), nthreads=16)
+        _check_equal(full[H - 1 - y], ref[H - 1 - y])
