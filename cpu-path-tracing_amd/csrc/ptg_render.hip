@@ -620,7 +620,7 @@ __device__ __forceinline__ bool bvh_done(const KArgs &A, int ni) { return (ni & 
 // Start a scan: the huge spheres (tested linearly, first), then the BVH in
 // the layout of the ray's direction octant.
 template <bool kCount>
-__device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
+__device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt, int oct_mask)
 {
     const float a = dot3(d, d);
     tr.tb = kInf;
@@ -632,7 +632,7 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 #if PTG_BVH_OCTANTS
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
-    tr.ni = (int)((oct & (unsigned)A.bvh_oct_mask) << A.bvh_shift);
+    tr.ni = (int)((oct & (unsigned)oct_mask) << A.bvh_shift);
 #else
     tr.ni = 0;
 #endif
@@ -663,9 +663,9 @@ __device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
 // One node step: test node tr.ni's box; hit -> descend (ni + 1; a leaf is
 // parked in tr.pend), miss -> skip the subtree.
 template <bool kCount>
-__device__ __forceinline__ void bvh_node_step(const KArgs &A, const SlabRay &r, BvhTrav &tr, ScanCount &cnt)
+__device__ __forceinline__ void bvh_node_step(const uint4 *qnodes, const SlabRay &r, BvhTrav &tr, ScanCount &cnt)
 {
-    const uint4 q = A.bvh_qnodes[tr.ni];  // one 16-B load
+    const uint4 q = qnodes[tr.ni];  // one 16-B load
     if constexpr (kCount)
         cnt.boxes += 1;
     const float tx1 = __builtin_fmaf((float)(q.x & 0xFFFFu), r.sx, r.bx);
@@ -706,10 +706,10 @@ template <bool kCount>
 __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest, ScanCount &cnt)
 {
     BvhTrav tr;
-    bvh_start<kCount>(A, o, d, tr, cnt);
+    bvh_start<kCount>(A, o, d, tr, cnt, A.bvh_oct_mask);
     const SlabRay sr = slab_ray(A, o, d);
     while (!bvh_done(A, tr.ni)) {
-        bvh_node_step<kCount>(A, sr, tr, cnt);
+        bvh_node_step<kCount>(A.bvh_qnodes, sr, tr, cnt);
         if (tr.pend >= 0)
             bvh_leaf<kCount>(A, o, d, tr, cnt);
     }
@@ -1017,7 +1017,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     };
     auto store_pre = [&](int it, f3 ro, f3 rd, uint32_t rs) {
         lds_pre[wv][lane][0] = make_float4(ro.x, ro.y, rd.x, rd.y);
-        lds_pre[wv][lane][1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), 0.0f);
+        // ro.z (= the camera's z, the lens offset has no z) rides in the
+        // record's last word: read back with the ray, not as a kernel
+        // argument (a scalar load + wait in the path-start block)
+        lds_pre[wv][lane][1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), ro.z);
     };
     if (item >= 0) {
         f3 ro, rd;
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         if (has_pre) {
             const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
             park();
-            begin(__float_as_int(p1.z), mk3(p0.x, p0.y, A.pos_z), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
+            begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
             has_pre = false;
         } else {
             waiting = true;  // E is kept until the batch
@@ -1126,13 +1129,21 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
         // of the active lanes) or none walks, shades the ready lanes.
         BvhTrav tr{0, -1, kInf, -1};  // started per segment by bvh_start
+        // kernel-argument pointers used in the loops, pinned in SGPRs once:
+        // left to the compiler they were re-loaded (s_load + wait) in every
+        // node step and every shade
+        const uint4 *qnodes = A.bvh_qnodes;
+        asm volatile("" : "+s"(qnodes));
+        asm volatile("" : "+s"(trig));
+        int oct_mask = A.bvh_oct_mask;
+        asm volatile("" : "+s"(oct_mask));
         for (;;) {
             if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
                 break;
             if (item >= 0 && phase == 0) {
                 if constexpr (kCount)
                     segs += 1;
-                bvh_start<kCount>(A, o, d, tr, scnt);
+                bvh_start<kCount>(A, o, d, tr, scnt, oct_mask);
                 phase = bvh_done(A, tr.ni) ? 2 : 1;
             }
             {
@@ -1167,7 +1178,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         if (trv && tr.pend >= 0)
                             bvh_leaf<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt);
                     } else if (trv && tr.pend < 0) {  // node step
-                        bvh_node_step<kCount && !PTG_WAVE_STATS>(A, sr, tr, scnt);
+                        bvh_node_step<kCount && !PTG_WAVE_STATS>(qnodes, sr, tr, scnt);
                     }
                     if (trv && tr.pend < 0 && bvh_done(A, tr.ni))
                         phase = 2;
@@ -1182,7 +1193,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
 #endif
             if (item >= 0 && phase == 2) {
                 phase = 0;
-                if (shade(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, A.trig, o, d, T, E, depth, st))
+                if (shade(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
             refill();
