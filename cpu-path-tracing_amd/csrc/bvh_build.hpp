@@ -279,31 +279,278 @@ struct BvhGrid {
     float lo[3], scale[3];
 };
 
+// 16-bit box quantiser on the root box's grid (shared by the binary and the
+// 4-wide layouts)
+struct BvhQuantiser {
+    double lo[3], sc[3];
+    BvhGrid grid;
+    explicit BvhQuantiser(const BvhNodeHost &root) : grid{}
+    {
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = root.bmin[c];
+            const double ext = (double)root.bmax[c] - lo[c];
+            sc[c] = ext > 0.0 ? ext / 65533.0 : 1e-30;
+            grid.lo[c] = (float)lo[c];
+            grid.scale[c] = (float)sc[c];
+        }
+    }
+    uint32_t qlo(double v, int c) const
+    {
+        return (uint32_t)std::clamp(std::floor((v - lo[c]) / sc[c]) - 1.0, 0.0, 65535.0);
+    }
+    uint32_t qhi(double v, int c) const
+    {
+        return (uint32_t)std::clamp(std::ceil((v - lo[c]) / sc[c]) + 1.0, 0.0, 65535.0);
+    }
+    // flip bit k: axis k's planes swapped (far plane in the "min" field),
+    // for rays with d_k < 0 -- the first field is then always the near plane
+    BvhNodeQ box(const BvhNodeHost &n, int32_t word, int flip = 0) const
+    {
+        uint32_t a[3], b[3];
+        for (int c = 0; c < 3; ++c) {
+            a[c] = qlo(n.bmin[c], c);
+            b[c] = qhi(n.bmax[c], c);
+            if ((flip >> c) & 1)
+                std::swap(a[c], b[c]);
+        }
+        BvhNodeQ q;
+        q.xy_min = a[0] | (a[1] << 16);
+        q.z_min_x_max = a[2] | (b[0] << 16);
+        q.y_max_z_max = b[1] | (b[2] << 16);
+        q.word = word;
+        return q;
+    }
+};
+
 inline BvhGrid quantise_bvh(const std::vector<BvhNodeHost> &nodes, std::vector<BvhNodeQ> &out)
 {
-    BvhGrid g{};
     out.resize(nodes.size());
     if (nodes.empty())
-        return g;
-    double lo[3], sc[3];
-    for (int c = 0; c < 3; ++c) {
-        lo[c] = nodes[0].bmin[c];
-        const double ext = (double)nodes[0].bmax[c] - lo[c];
-        sc[c] = ext > 0.0 ? ext / 65533.0 : 1e-30;
-        g.lo[c] = (float)lo[c];
-        g.scale[c] = (float)sc[c];
-    }
-    auto qlo = [&](double v, int c) { return (uint32_t)std::clamp(std::floor((v - lo[c]) / sc[c]) - 1.0, 0.0, 65535.0); };
-    auto qhi = [&](double v, int c) { return (uint32_t)std::clamp(std::ceil((v - lo[c]) / sc[c]) + 1.0, 0.0, 65535.0); };
+        return BvhGrid{};
+    const BvhQuantiser z(nodes[0]);
     for (size_t i = 0; i < nodes.size(); ++i) {
         const BvhNodeHost &n = nodes[i];
-        BvhNodeQ &q = out[i];
-        q.xy_min = qlo(n.bmin[0], 0) | (qlo(n.bmin[1], 1) << 16);
-        q.z_min_x_max = qlo(n.bmin[2], 2) | (qhi(n.bmax[0], 0) << 16);
-        q.y_max_z_max = qhi(n.bmax[1], 1) | (qhi(n.bmax[2], 2) << 16);
-        q.word = n.leaf >= 0 ? (int32_t)(0x80000000u | (uint32_t)n.leaf) : n.skip;
+        out[i] = z.box(n, n.leaf >= 0 ? (int32_t)(0x80000000u | (uint32_t)n.leaf) : n.skip);
     }
-    return g;
+    return z.grid;
+}
+
+// IEEE binary16 on the host (the wide layout's box planes): value of a bit
+// pattern, and the largest / smallest finite half <= / >= a double.
+inline double half_value(uint16_t h)
+{
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const double v = e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(1024 + m), e - 25);
+    return (h & 0x8000u) ? -v : v;
+}
+inline const std::vector<std::pair<double, uint16_t>> &half_table()
+{
+    static const std::vector<std::pair<double, uint16_t>> t = [] {
+        std::vector<std::pair<double, uint16_t>> v;
+        for (uint32_t h = 0; h < 65536; ++h)
+            if (((h >> 10) & 31) != 31 && h != 0x8000u)  // finite, one zero
+                v.emplace_back(half_value((uint16_t)h), (uint16_t)h);
+        std::sort(v.begin(), v.end());
+        return v;
+    }();
+    return t;
+}
+inline uint16_t half_floor(double x)
+{
+    const auto &t = half_table();
+    auto it = std::upper_bound(t.begin(), t.end(), std::make_pair(x, (uint16_t)0xFFFF));
+    return it == t.begin() ? t.front().second : std::prev(it)->second;
+}
+inline uint16_t half_ceil(double x)
+{
+    const auto &t = half_table();
+    auto it = std::lower_bound(t.begin(), t.end(), std::make_pair(x, (uint16_t)0));
+    return it == t.end() ? t.back().second : it->second;
+}
+
+// 4-wide tree (ptg_render.hip PTG_BVH_WIDE): each wide node is 4 consecutive
+// 16-B records (one 64-B line), one per child -- the child's box and a word:
+// >= 0 the child node's first record, < 0 a leaf (INT_MIN | count << 24 |
+// first).  Box planes are binary16 values on a grid centred on the root box
+// (plane = centre + h * scale, |h| <= 30000, rounded outward), so the kernel
+// reads each one with a single v_fma_mix_f32 (no integer convert): words
+// {near x, near y}, {near z, far x}, {far y, far z}, low half first.  The
+// layout of octant k stores each box near-plane first for rays of that
+// octant (axis c swapped when bit c of k is set).  Unused slots hold an empty
+// leaf (count 0) whose box the octant's rays always miss (near plane beyond
+// the far plane).  A wide node collapses up to three binary levels: starting
+// from a binary node's two children it repeatedly opens the inner child with
+// the largest surface, in place, so the children keep the binary tree's
+// near-first order for the octant (order_bvh).  Nodes are in depth-first
+// pre-order (a node's children follow it).
+constexpr int kWide = 4;
+constexpr int32_t kWideEmpty = (int32_t)0x80000000u;
+
+struct WideGrid {
+    float centre[3], scale[3];
+    explicit WideGrid(const BvhNodeHost &root)
+    {
+        for (int c = 0; c < 3; ++c) {
+            const double half = 0.5 * ((double)root.bmax[c] - (double)root.bmin[c]);
+            centre[c] = (float)(0.5 * ((double)root.bmax[c] + (double)root.bmin[c]));
+            scale[c] = half > 0.0 ? (float)(half / 30000.0) : 1e-30f;
+        }
+    }
+    // plane value v in grid units, rounded outward (dir -1: down, +1: up),
+    // checked against the decoded plane centre + h * scale
+    uint16_t plane(double v, int c, int dir) const
+    {
+        const double g = (v - (double)centre[c]) / (double)scale[c];
+        uint16_t h = dir < 0 ? half_floor(g) : half_ceil(g);
+        for (int k = 0; k < 4; ++k) {  // one more half step out while the decoded plane is inside
+            const double back = (double)centre[c] + half_value(h) * (double)scale[c];
+            if (dir < 0 ? back <= v : back >= v)
+                break;
+            h = dir < 0 ? half_floor(std::nextafter(half_value(h), -INFINITY))
+                        : half_ceil(std::nextafter(half_value(h), INFINITY));
+        }
+        return h;
+    }
+    BvhNodeQ box(const BvhNodeHost &n, int32_t word, int flip) const
+    {
+        uint32_t a[3], b[3];
+        for (int c = 0; c < 3; ++c) {
+            a[c] = plane(n.bmin[c], c, -1);
+            b[c] = plane(n.bmax[c], c, +1);
+            if ((flip >> c) & 1)
+                std::swap(a[c], b[c]);
+        }
+        BvhNodeQ q;
+        q.xy_min = a[0] | (a[1] << 16);
+        q.z_min_x_max = a[2] | (b[0] << 16);
+        q.y_max_z_max = b[1] | (b[2] << 16);
+        q.word = word;
+        return q;
+    }
+    BvhNodeQ empty(int flip) const
+    {
+        uint32_t a[3], b[3];
+        for (int c = 0; c < 3; ++c) {
+            const bool f = (flip >> c) & 1;
+            a[c] = f ? 0xFB53u : 0x7B53u;  // near plane -/+60000 and far plane +/-60000: the
+            b[c] = f ? 0x7B53u : 0xFB53u;  // octant's rays enter the slab after leaving it
+        }
+        BvhNodeQ q;
+        q.xy_min = a[0] | (a[1] << 16);
+        q.z_min_x_max = a[2] | (b[0] << 16);
+        q.y_max_z_max = b[1] | (b[2] << 16);
+        q.word = kWideEmpty;
+        return q;
+    }
+};
+
+namespace detail {
+
+inline void wide_children(const BvhBuild &b, int i, int octant, int kids[kWide], int &nk)
+{
+    auto ordered = [&](int node, int &first, int &second) {
+        const int lo = node + 1, hi = b.nodes[lo].skip;
+        const bool flip = (octant >> b.axis[node]) & 1;
+        first = flip ? hi : lo;
+        second = flip ? lo : hi;
+    };
+    nk = 2;
+    ordered(i, kids[0], kids[1]);
+    while (nk < kWide) {
+        int pick = -1;
+        double best = -1.0;
+        for (int k = 0; k < nk; ++k) {
+            const BvhNodeHost &c = b.nodes[kids[k]];
+            if (c.leaf >= 0)
+                continue;
+            double mn[3], mx[3];
+            for (int a = 0; a < 3; ++a) {
+                mn[a] = c.bmin[a];
+                mx[a] = c.bmax[a];
+            }
+            const double area = half_area(mn, mx);
+            if (area > best) {
+                best = area;
+                pick = k;
+            }
+        }
+        if (pick < 0)
+            break;
+        int f, s;
+        ordered(kids[pick], f, s);
+        for (int k = nk; k > pick + 1; --k)
+            kids[k] = kids[k - 1];
+        kids[pick] = f;
+        kids[pick + 1] = s;
+        ++nk;
+    }
+}
+
+// emits binary node i (inner) as a wide node at out.size(); returns its first record
+inline int wide_rec(const BvhBuild &b, int i, int octant, const WideGrid &z, int32_t base,
+                    std::vector<BvhNodeQ> &out)
+{
+    const int me = (int)out.size();
+    int kids[kWide], nk = 0;
+    if (b.nodes[i].leaf >= 0) {  // a one-leaf tree: the root node holds the leaf
+        kids[0] = i;
+        nk = 1;
+    } else {
+        wide_children(b, i, octant, kids, nk);
+    }
+    out.resize(me + kWide);
+    for (int k = nk; k < kWide; ++k)
+        out[me + k] = z.empty(octant);
+    for (int k = 0; k < nk; ++k) {
+        const BvhNodeHost &c = b.nodes[kids[k]];
+        int32_t word;
+        if (c.leaf >= 0)
+            word = (int32_t)(0x80000000u | (uint32_t)c.leaf);
+        else
+            word = base + wide_rec(b, kids[k], octant, z, base, out);
+        out[me + k] = z.box(c, word, octant);
+    }
+    return me;
+}
+
+inline void wide_conts_rec(const std::vector<BvhNodeQ> &w, int32_t base, int node, int32_t cont,
+                           std::vector<int32_t> &out)
+{
+    out[node / kWide] = cont;
+    int used = 0;
+    while (used < kWide && w[node + used].word != kWideEmpty)
+        ++used;
+    for (int k = 0; k < used; ++k)
+        if (w[node + k].word >= 0)
+            wide_conts_rec(w, base, w[node + k].word - base, k + 1 < used ? base + node + k + 1 : cont, out);
+}
+
+}  // namespace detail
+
+// The 4-wide layout of the tree for rays of one direction octant; record
+// words are offset by `base` (the layout's position in the device array).
+// Empty for an empty tree.
+inline std::vector<BvhNodeQ> wide_bvh(const BvhBuild &b, int octant, int32_t base)
+{
+    std::vector<BvhNodeQ> out;
+    if (b.nodes.empty())
+        return out;
+    const WideGrid z(b.nodes[0]);
+    detail::wide_rec(b, 0, octant, z, base, out);
+    return out;
+}
+
+// Continuations of a wide layout, one per node (first record / 4): the
+// position after the node's subtree in depth-first order -- the parent's
+// first record + the next used slot (the walk resumes the parent from that
+// slot), else the parent's continuation; -1 after the root.  The kernel's
+// short stack falls back on them when it overflows.
+inline std::vector<int32_t> wide_conts(const std::vector<BvhNodeQ> &w, int32_t base)
+{
+    std::vector<int32_t> out(w.size() / kWide, -1);
+    if (!w.empty())
+        detail::wide_conts_rec(w, base, 0, -1, out);
+    return out;
 }
 
 }  // namespace ptg

@@ -121,6 +121,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_OCTANTS
 #define PTG_BVH_OCTANTS 1  // BVH: one depth-first layout per ray-direction octant (near child first)
 #endif
+#ifndef PTG_BVH_WIDE
+#define PTG_BVH_WIDE 1  // BVH: 4-wide nodes walked with a per-lane short stack (0: binary stackless skip walk)
+#endif
 #ifndef PTG_BVH_TAIL_MIN_HALF_ROUNDS
 #define PTG_BVH_TAIL_MIN_HALF_ROUNDS 6  // BVH scenes: split tail from 3 rounds of wave slots on
 #endif
@@ -216,7 +219,7 @@ struct KArgs {
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
     const uint4 *bvh_qnodes;  // the same nodes, compact (bvh_build.hpp BvhNodeQ; render kernel)
-    float q_lo[3], q_scale[3];
+    float q_lo[3], q_scale[3];  // box grid: plane = q_lo + value * q_scale (binary: u16 values; wide: binary16)
     const float4 *bvh_sph;    // leaf-ordered spheres {C, -R^2} (BVH leaves hold only non-huge spheres)
     const int *bvh_id;        // leaf-ordered scene indices
     const GeoRec *big_geo;    // huge spheres, tested linearly
@@ -227,6 +230,7 @@ struct KArgs {
     // a walk is done when (ni & bvh_mask) reaches n_nodes
     int bvh_shift, bvh_mask;
     int bvh_oct_mask;  // direction-sign bits that select the layout (x 1, y 2, z 4): bvh_octant_mask
+    const int *bvh_cont;  // PTG_BVH_WIDE: per wide node (first record / 4) its continuation (bvh_build.hpp wide_conts)
     const float2 *trig;  // {cos, sin}(2 pi k / 128), staged in LDS (sincos2pi_tab)
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
     float pos_x, pos_y, pos_z;
@@ -608,14 +612,51 @@ __device__ __forceinline__ void update_lex(const float t, const int sid, float &
 // their next segment while the wave keeps walking for the long rays -- a
 // wave otherwise waits for its slowest ray (measured 93 wave-level node
 // steps for 33 per ray on the 10,000-sphere scene).
+// global (address space 1) pointers: kernel-argument pointers pinned in
+// SGPRs lose their address space, and generic (flat) loads also wait on LDS
+template <class T>
+using gptr = const T __attribute__((address_space(1))) *;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // a compact node record, loadable from gptr
+
 struct BvhTrav {
-    int ni;    // next node in depth-first order (bvh_done: walk finished)
+    int ni;    // binary: next node in depth-first order; wide: see below
     int pend;  // parked leaf (first | count << 24) or -1
     float tb;  // nearest root so far
     int best;  // winner's scene index or -1
+#if PTG_BVH_WIDE
+    // wide walk: ni = the next position (a wide node's first record + the
+    // slot to resume from, >= 0), a leaf word (< -1, parked at the next
+    // chance) or -1 (walk finished).  A two-entry stack (top first, -1 empty)
+    // of positions / leaf words still to visit; when it overflows it is
+    // cleared and the walk continues, once it runs dry, from the resume
+    // position `res` and its continuation chain (bvh_build.hpp wide_conts:
+    // everything after it in depth-first order, culled by tb), so any tree
+    // depth is walked correctly with three registers.
+    int s0, s1;
+    int res;
+#endif
 };
 
-__device__ __forceinline__ bool bvh_done(const KArgs &A, int ni) { return (ni & A.bvh_mask) >= A.n_nodes; }
+#if PTG_BVH_WIDE
+__device__ __forceinline__ bool bvh_done(const KArgs &, const BvhTrav &tr) { return tr.ni == -1 && tr.pend < 0; }
+__device__ __forceinline__ int bvh_pop(gptr<int> cont, BvhTrav &tr)
+{
+    const int v = tr.s0;
+    tr.s0 = tr.s1;
+    tr.s1 = -1;
+    if (v != -1)
+        return v;
+    const int r = tr.res;  // stack dry: the resume position, then its continuation
+    if (r != -1)
+        tr.res = cont[r >> 2];
+    return r;
+}
+#else
+__device__ __forceinline__ bool bvh_done(const KArgs &A, const BvhTrav &tr)
+{
+    return tr.pend < 0 && (tr.ni & A.bvh_mask) >= A.n_nodes;
+}
+#endif
 
 // Start a scan: the huge spheres (tested linearly, first), then the BVH in
 // the layout of the ray's direction octant.
@@ -629,7 +670,17 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
         update_lex(root_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
-#if PTG_BVH_OCTANTS
+#if PTG_BVH_WIDE
+    // the wide layouts store each box near-plane first for their octant:
+    // all 8 layouts exist (bvh_oct_mask = 7)
+    const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
+                         ((__float_as_uint(d.z) >> 29) & 4u);
+    tr.ni = A.n_nodes > 0 ? (int)(oct << A.bvh_shift) : -1;
+    tr.s0 = -1;
+    tr.s1 = -1;
+    tr.res = -1;
+    (void)oct_mask;
+#elif PTG_BVH_OCTANTS
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
     tr.ni = (int)((oct & (unsigned)oct_mask) << A.bvh_shift);
@@ -660,14 +711,10 @@ __device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
     return r;
 }
 
-// One node step: test node tr.ni's box; hit -> descend (ni + 1; a leaf is
-// parked in tr.pend), miss -> skip the subtree.
-template <bool kCount>
-__device__ __forceinline__ void bvh_node_step(const uint4 *qnodes, const SlabRay &r, BvhTrav &tr, ScanCount &cnt)
+// Box test of one compact record (culling only): slab entry/exit in grid
+// units, padded.
+__device__ __forceinline__ bool box_hit(const u32x4 q, const SlabRay &r, const float tcap)
 {
-    const uint4 q = qnodes[tr.ni];  // one 16-B load
-    if constexpr (kCount)
-        cnt.boxes += 1;
     const float tx1 = __builtin_fmaf((float)(q.x & 0xFFFFu), r.sx, r.bx);
     const float ty1 = __builtin_fmaf((float)(q.x >> 16), r.sy, r.by);
     const float tz1 = __builtin_fmaf((float)(q.y & 0xFFFFu), r.sz, r.bz);
@@ -677,16 +724,102 @@ __device__ __forceinline__ void bvh_node_step(const uint4 *qnodes, const SlabRay
     const float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
                                        __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
     const float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
-                                        __builtin_fminf(__builtin_fmaxf(tz1, tz2), tr.tb * 1.0001f));
-    const bool hit = !(t_in > t_out * 1.0001f + 1e-6f);
+                                        __builtin_fminf(__builtin_fmaxf(tz1, tz2), tcap));
+    return !(t_in > t_out * 1.0001f + 1e-6f);
+}
+
+#if PTG_BVH_WIDE
+// Box test of a wide-layout record: binary16 planes on the wide grid, stored
+// near-plane first for the ray's octant (bvh_build.hpp WideGrid), each read
+// by one v_fma_mix_f32.  No slab margin: the boxes are padded far beyond the
+// rounding of the slab times (bvh_build.hpp); tcap keeps the 1e-4 margin
+// over the nearest root.
+// binary16 halves of a word as float: folded into v_fma_mix_f32 operands.
+// (A __builtin_bit_cast of the word to a 2 x _Float16 vector miscompiles
+// here: every plane was read from the record's first word.)
+__device__ __forceinline__ float lo_half(unsigned w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
+__device__ __forceinline__ float hi_half(unsigned w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
+__device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, const float tcap)
+{
+    const float tnx = __builtin_fmaf(lo_half(q.x), r.sx, r.bx);
+    const float tny = __builtin_fmaf(hi_half(q.x), r.sy, r.by);
+    const float tnz = __builtin_fmaf(lo_half(q.y), r.sz, r.bz);
+    const float tfx = __builtin_fmaf(hi_half(q.y), r.sx, r.bx);
+    const float tfy = __builtin_fmaf(lo_half(q.z), r.sy, r.by);
+    const float tfz = __builtin_fmaf(hi_half(q.z), r.sz, r.bz);
+    const float t_in = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, 0.0f));
+    const float t_out = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, tcap));
+    return !(t_in > t_out);
+}
+
+// One wide node step at position ni (node + first slot): the node's 4
+// records (one 64-B line) in one go; the nearest hit child (slots are in
+// near-first order for the layout's octant) is visited next; one more hit
+// goes on the stack as itself, several as the position of the second (the
+// node is re-tested from there, with the culling distance of then); a hit
+// leaf is parked in tr.pend.  A leaf word from the stack is parked without a
+// load.  Selections are branch-free (v_cndmask).
+template <bool kCount>
+__device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
+                                              ScanCount &cnt)
+{
+    int next = tr.ni;  // a leaf word from the stack, or -1
+    if (tr.ni >= 0) {
+        const int base = tr.ni & ~3;
+        gptr<u32x4> q = qnodes + base;
+        const u32x4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        if constexpr (kCount)
+            cnt.boxes += 4 - (tr.ni & 3);
+        const float tcap = tr.tb * 1.0001f;
+        const unsigned m = ((box_hit_sorted(q0, r, tcap) ? 1u : 0u) | (box_hit_sorted(q1, r, tcap) ? 2u : 0u) |
+                            (box_hit_sorted(q2, r, tcap) ? 4u : 0u) | (box_hit_sorted(q3, r, tcap) ? 8u : 0u)) &
+                           (0xFu << (tr.ni & 3));
+        // the word of the lowest set bit of x (x != 0)
+        auto lowest = [&](unsigned x) {
+            int w = (int)q3.w;
+            w = (x & 4u) ? (int)q2.w : w;
+            w = (x & 2u) ? (int)q1.w : w;
+            return (x & 1u) ? (int)q0.w : w;
+        };
+        next = m != 0u ? lowest(m) : -1;
+        const unsigned rest = m & (m - 1u);
+        const int pos = base + (int)__builtin_ctz(rest | 16u);
+        const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
+        const bool push = rest != 0u, full = tr.s1 != -1;
+        tr.res = (push && full) ? pos : tr.res;
+        const int s0 = tr.s0;
+        tr.s0 = push ? (full ? -1 : e) : s0;
+        tr.s1 = push ? (full ? -1 : s0) : tr.s1;
+    }
+    if (next == -1)
+        next = bvh_pop(cont, tr);
+    if (next < -1) {
+        tr.pend = next & 0x7FFFFFFF;
+        next = bvh_pop(cont, tr);
+    }
+    tr.ni = next;
+}
+#else
+// One node step: test node tr.ni's box; hit -> descend (ni + 1; a leaf is
+// parked in tr.pend), miss -> skip the subtree.
+template <bool kCount>
+__device__ __forceinline__ void bvh_node_step(gptr<int>, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
+                                              ScanCount &cnt)
+{
+    const u32x4 q = qnodes[tr.ni];  // one 16-B load
+    if constexpr (kCount)
+        cnt.boxes += 1;
+    const bool hit = box_hit(q, r, tr.tb * 1.0001f);
     const int w = (int)q.w;  // >= 0 inner node's skip; < 0 leaf (its skip is the next node)
     tr.pend = (hit && w < 0) ? (w & 0x7FFFFFFF) : -1;
     tr.ni = (hit || w < 0) ? tr.ni + 1 : w;
 }
+#endif
 
-// The parked leaf's spheres: compact records {C, -R^2} in leaf order.
+// The parked leaf's spheres: compact records {C, -R^2} in leaf order.  Wide
+// walk: a leaf word waiting in tr.ni is parked next.
 template <bool kCount>
-__device__ __forceinline__ void bvh_leaf(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
+__device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
     const float a = dot3(d, d);
     const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
@@ -698,6 +831,14 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, f3 o, f3 d, BvhTrav &tr
             update_lex(t, A.bvh_id[first + j], tr.tb, tr.best);
     }
     tr.pend = -1;
+#if PTG_BVH_WIDE
+    if (tr.ni < -1) {
+        tr.pend = tr.ni & 0x7FFFFFFF;
+        tr.ni = bvh_pop(cont, tr);
+    }
+#else
+    (void)cont;
+#endif
 }
 
 // Whole scan of one ray (parity probe kernel): walk, testing each parked leaf
@@ -708,10 +849,11 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     BvhTrav tr;
     bvh_start<kCount>(A, o, d, tr, cnt, A.bvh_oct_mask);
     const SlabRay sr = slab_ray(A, o, d);
-    while (!bvh_done(A, tr.ni)) {
-        bvh_node_step<kCount>(A.bvh_qnodes, sr, tr, cnt);
+    while (!bvh_done(A, tr)) {
         if (tr.pend >= 0)
-            bvh_leaf<kCount>(A, o, d, tr, cnt);
+            bvh_leaf<kCount>(A, (gptr<int>)A.bvh_cont, o, d, tr, cnt);
+        else
+            bvh_node_step<kCount>((gptr<int>)A.bvh_cont, (gptr<u32x4>)A.bvh_qnodes, sr, tr, cnt);
     }
     tbest = tr.tb;
     return tr.best;
@@ -1128,12 +1270,14 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // or ready (scan done, to be shaded); an iteration starts the fresh
         // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
         // of the active lanes) or none walks, shades the ready lanes.
-        BvhTrav tr{0, -1, kInf, -1};  // started per segment by bvh_start
+        BvhTrav tr{};  // started per segment by bvh_start
         // kernel-argument pointers used in the loops, pinned in SGPRs once:
         // left to the compiler they were re-loaded (s_load + wait) in every
         // node step and every shade
-        const uint4 *qnodes = A.bvh_qnodes;
+        gptr<u32x4> qnodes = (gptr<u32x4>)A.bvh_qnodes;
         asm volatile("" : "+s"(qnodes));
+        gptr<int> cont = (gptr<int>)A.bvh_cont;
+        asm volatile("" : "+s"(cont));
         asm volatile("" : "+s"(trig));
         int oct_mask = A.bvh_oct_mask;
         asm volatile("" : "+s"(oct_mask));
@@ -1143,8 +1287,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if (item >= 0 && phase == 0) {
                 if constexpr (kCount)
                     segs += 1;
-                bvh_start<kCount>(A, o, d, tr, scnt, oct_mask);
-                phase = bvh_done(A, tr.ni) ? 2 : 1;
+                bvh_start<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt, oct_mask);
+                phase = bvh_done(A, tr) ? 2 : 1;
             }
             {
                 const SlabRay sr = slab_ray(A, o, d);
@@ -1176,11 +1320,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         // ds_bpermute + LDS atomicMin measured 1.7 % slower: the leaf
                         // tests are cheap next to the node steps' memory latency)
                         if (trv && tr.pend >= 0)
-                            bvh_leaf<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt);
+                            bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
                     } else if (trv && tr.pend < 0) {  // node step
-                        bvh_node_step<kCount && !PTG_WAVE_STATS>(qnodes, sr, tr, scnt);
+                        bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
                     }
-                    if (trv && tr.pend < 0 && bvh_done(A, tr.ni))
+                    if (trv && bvh_done(A, tr))
                         phase = 2;
                 }
             }
@@ -2009,15 +2153,32 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
         const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
-        int shift = 0;  // layout stride: a power of two > n_nodes
-        while ((size_t(1) << shift) <= n_nodes)
+#if PTG_BVH_WIDE
+        const size_t n_recs = wide_bvh(b, 0, 0).size();  // records per layout
+#else
+        const size_t n_recs = n_nodes;
+#endif
+        int shift = 0;  // layout stride: a power of two > n_recs
+        while ((size_t(1) << shift) <= n_recs)
             ++shift;
-        const size_t stride = size_t(1) << shift, n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
-        const size_t total = off_q + n_layouts * stride * sizeof(BvhNodeQ) + 16;
+#if PTG_BVH_WIDE
+        const size_t n_layouts = 8;  // near-plane-first boxes: one layout per octant
+#else
+        const size_t n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
+#endif
+        const size_t stride = size_t(1) << shift;
+        const size_t off_cont = off_q + n_layouts * stride * sizeof(BvhNodeQ);
+        const size_t total = off_cont + (PTG_BVH_WIDE ? n_layouts * stride / kWide * sizeof(int32_t) : 0) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
         for (size_t k = 0; k < n_layouts; ++k) {
             std::vector<BvhNodeQ> qk;
+#if PTG_BVH_WIDE
+            qk = wide_bvh(b, (int)k, (int32_t)(k * stride));  // same root box: same grid, absolute words
+            const std::vector<int32_t> ck = wide_conts(qk, (int32_t)(k * stride));
+            std::memcpy(blob.data() + off_cont + k * (stride / kWide) * sizeof(int32_t), ck.data(),
+                        ck.size() * sizeof(int32_t));
+#else
             if (k == 0)
                 qk = qn;
             else
@@ -2025,15 +2186,25 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             for (BvhNodeQ &z : qk)
                 if (z.word >= 0)
                     z.word += (int32_t)(k * stride);  // absolute skip index
-            std::memcpy(blob.data() + off_q + k * stride * sizeof(BvhNodeQ), qk.data(), n_nodes * sizeof(BvhNodeQ));
+#endif
+            std::memcpy(blob.data() + off_q + k * stride * sizeof(BvhNodeQ), qk.data(), n_recs * sizeof(BvhNodeQ));
         }
         A.bvh_shift = shift;
         A.bvh_mask = (int)(stride - 1);
-        A.bvh_oct_mask = PTG_BVH_OCTANTS ? bvh_octant_mask(b) : 0;
+        A.bvh_oct_mask = PTG_BVH_WIDE ? 7 : PTG_BVH_OCTANTS ? bvh_octant_mask(b) : 0;
+#if PTG_BVH_WIDE
+        const WideGrid wg(b.nodes.empty() ? BvhNodeHost{} : b.nodes[0]);
+        for (int c = 0; c < 3; ++c) {
+            A.q_lo[c] = wg.centre[c];
+            A.q_scale[c] = wg.scale[c];
+        }
+        (void)grid;
+#else
         for (int c = 0; c < 3; ++c) {
             A.q_lo[c] = grid.lo[c];
             A.q_scale[c] = grid.scale[c];
         }
+#endif
         for (size_t i = 0; i < n_leaf; ++i) {
             const ptg_sphere &sp = spheres[b.order[i]];  // leaf record {C, -R^2}, as the GeoRec of a small sphere
             const float4 rec = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2],
@@ -2053,11 +2224,12 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         unsigned char *base = static_cast<unsigned char *>(ctx->d_bvh);
         A.bvh_nodes = reinterpret_cast<const float4 *>(base);
         A.bvh_qnodes = reinterpret_cast<const uint4 *>(base + off_q);
+        A.bvh_cont = reinterpret_cast<const int *>(base + off_cont);
         A.bvh_sph = reinterpret_cast<const float4 *>(base + off_geo);
         A.bvh_id = reinterpret_cast<const int *>(base + off_id);
         A.big_geo = reinterpret_cast<const GeoRec *>(base + off_bgeo);
         A.big_id = reinterpret_cast<const int *>(base + off_bid);
-        A.n_nodes = (int)n_nodes;
+        A.n_nodes = (int)n_recs;
         A.n_big = (int)n_big;
     }
     A.pos_x = (float)cam->position[0];

@@ -8,7 +8,11 @@
 //     node after the first child's subtree;
 //   * every box contains its subtree's spheres (centre +- radius) and its
 //     children's boxes (culling can never drop a candidate);
-//   * the 16-bit quantised boxes, decoded on the grid, contain the float boxes.
+//   * the 16-bit quantised boxes, decoded on the grid, contain the float boxes;
+//   * the 4-wide layouts (wide_bvh, PTG_BVH_WIDE): 4 records per node in
+//     pre-order, every leaf reached exactly once from the root, each record's
+//     decoded box contains its subtree's spheres, empty slots are count-0
+//     leaves, and the children keep the binary tree's near-first order.
 // Prints "ok <nodes>" per scene; exits non-zero on the first violation.
 #include <cmath>
 #include <cstdio>
@@ -67,6 +71,115 @@ static void check_layout(const std::vector<ptg_sphere> &s, const BvhBuild &b, co
         CHECK(leaf_cover[k] == 1, "octant %d leaf slot %zu covered %d times", octant, k, leaf_cover[k]);
 }
 
+// decoded box of a wide record (binary16 planes on the wide grid), in scene units
+static void decode(const WideGrid &g, const BvhNodeQ &z, double lo[3], double hi[3])
+{
+    const uint16_t qv[6] = {(uint16_t)(z.xy_min & 0xFFFFu), (uint16_t)(z.xy_min >> 16),
+                            (uint16_t)(z.z_min_x_max & 0xFFFFu), (uint16_t)(z.z_min_x_max >> 16),
+                            (uint16_t)(z.y_max_z_max & 0xFFFFu), (uint16_t)(z.y_max_z_max >> 16)};
+    for (int c = 0; c < 3; ++c) {  // stored near-first: swapped for d_c < 0
+        const double a = g.centre[c] + half_value(qv[c]) * (double)g.scale[c];
+        const double b = g.centre[c] + half_value(qv[3 + c]) * (double)g.scale[c];
+        lo[c] = std::min(a, b);
+        hi[c] = std::max(a, b);
+    }
+}
+
+// walks wide node `node` (first record index, layout-relative): marks the
+// leaves it reaches, checks boxes; returns the spheres' slots of its subtree
+static void wide_walk(const std::vector<ptg_sphere> &s, const BvhBuild &b, const WideGrid &g,
+                      const std::vector<BvhNodeQ> &w, int32_t base, int node, std::vector<int> &cover,
+                      std::vector<int> &slots, int octant)
+{
+    CHECK(node >= 0 && node % kWide == 0 && node + kWide <= (int)w.size(), "octant %d wide node %d", octant, node);
+    int used = 0;
+    for (int k = 0; k < kWide; ++k) {
+        const BvhNodeQ &r = w[node + k];
+        std::vector<int> sub;
+        if (r.word == kWideEmpty) {
+            const BvhNodeQ e = g.empty(octant);
+            CHECK(r.xy_min == e.xy_min && r.z_min_x_max == e.z_min_x_max && r.y_max_z_max == e.y_max_z_max,
+                  "octant %d empty slot box", octant);
+            continue;
+        }
+        CHECK(used == k, "octant %d node %d: empty slot before child %d", octant, node, k);
+        ++used;
+        if (r.word < 0) {
+            const int leaf = r.word & 0x7FFFFFFF, first = leaf & 0xFFFFFF, cnt = leaf >> 24;
+            CHECK(cnt >= 1 && cnt <= kLeafSize && first + cnt <= (int)b.order.size(), "octant %d wide leaf", octant);
+            for (int j = first; j < first + cnt; ++j) {
+                cover[j] += 1;
+                sub.push_back(j);
+            }
+        } else {
+            const int child = r.word - base;
+            CHECK(child > node, "octant %d node %d child %d not after it (pre-order)", octant, node, child);
+            wide_walk(s, b, g, w, base, child, cover, sub, octant);
+            if (fails)
+                return;
+        }
+        double lo[3], hi[3];
+        decode(g, r, lo, hi);
+        const double near_x = half_value((uint16_t)(r.xy_min & 0xFFFFu)), far_x = half_value((uint16_t)(r.z_min_x_max >> 16));
+        CHECK((octant & 1) ? near_x >= far_x : near_x <= far_x, "octant %d: x planes not near-first", octant);
+        for (int j : sub) {
+            const ptg_sphere &sp = s[b.order[j]];
+            for (int c = 0; c < 3; ++c)
+                CHECK(lo[c] <= sp.position[c] - sp.radius && hi[c] >= sp.position[c] + sp.radius,
+                      "octant %d node %d slot %d does not contain sphere %d", octant, node, k, b.order[j]);
+        }
+        slots.insert(slots.end(), sub.begin(), sub.end());
+    }
+    CHECK(used >= 1, "octant %d node %d has no children", octant, node);
+}
+
+static void check_wide(const std::vector<ptg_sphere> &s, const BvhBuild &b)
+{
+    const WideGrid g(b.nodes[0]);
+    for (int oct = 0; oct < 8 && !fails; ++oct) {
+        const int32_t base = 1000 * oct;
+        const std::vector<BvhNodeQ> w = wide_bvh(b, oct, base);
+        CHECK(w.size() % kWide == 0 && !w.empty(), "octant %d: %zu wide records", oct, w.size());
+        std::vector<int> cover(b.order.size(), 0), slots;
+        wide_walk(s, b, g, w, base, 0, cover, slots, oct);
+        for (size_t k = 0; k < cover.size() && !fails; ++k)
+            CHECK(cover[k] == 1, "octant %d wide: leaf slot %zu reached %d times", oct, k, cover[k]);
+        // continuations: a walk that enters every child and moves on only by
+        // next-slot / continuation (the kernel's overflow fallback) reaches
+        // every leaf once, in depth-first order
+        if (!fails) {
+            const std::vector<int32_t> cont = wide_conts(w, base);
+            CHECK(cont.size() == w.size() / kWide && cont[0] == -1, "octant %d: continuation array", oct);
+            std::vector<int> order;
+            int32_t p = base, guard = 0;
+            while (p != -1 && !fails && ++guard < 10 * (int)w.size()) {
+                const int rel = p - base, node = rel & ~3, slot = rel & 3;
+                CHECK(rel >= 0 && rel < (int)w.size() && w[rel].word != kWideEmpty, "octant %d: position %d", oct, p);
+                const int32_t word = w[rel].word;
+                if (word >= 0) {
+                    p = word;
+                    continue;
+                }
+                const int leaf = word & 0x7FFFFFFF;
+                for (int j = 0; j < (leaf >> 24); ++j)
+                    order.push_back((leaf & 0xFFFFFF) + j);
+                p = slot + 1 < kWide && w[node + slot + 1].word != kWideEmpty ? p + 1 : cont[node / kWide];
+            }
+            CHECK(order == slots, "octant %d: continuation walk order", oct);
+        }
+        // near-first order: the binary layout of this octant visits the leaves
+        // in the same order as the wide walk's depth-first child order
+        if (!fails) {
+            std::vector<int> bin;
+            for (const BvhNodeHost &nd : order_bvh(b, oct))
+                if (nd.leaf >= 0)
+                    for (int j = 0; j < (nd.leaf >> 24); ++j)
+                        bin.push_back((nd.leaf & 0xFFFFFF) + j);
+            CHECK(bin == slots, "octant %d: wide child order differs from the binary near-first order", oct);
+        }
+    }
+}
+
 static void check_scene(const std::vector<ptg_sphere> &s)
 {
     const int n = (int)s.size();
@@ -123,9 +236,12 @@ static void check_scene(const std::vector<ptg_sphere> &s)
         else
             CHECK(z.word == nd.skip, "quantised skip %d", i);
     }
+    check_wide(s, b);
+    if (fails)
+        return;
     const int mask = bvh_octant_mask(b);
     CHECK(nn <= 1 || (mask >= 0 && mask <= 7), "octant mask %d", mask);
-    std::printf("ok %d spheres %d nodes %zu huge, 8 octant layouts, octant mask %d\n", n, nn, b.big.size(), mask);
+    std::printf("ok %d spheres %d nodes %zu huge, 8 octant layouts (binary and 4-wide), octant mask %d\n", n, nn, b.big.size(), mask);
 }
 
 int main()

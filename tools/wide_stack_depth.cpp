@@ -1,0 +1,273 @@
+// Stack depth of the 4-wide BVH walk (ptg_render.hip PTG_BVH_WIDE) on a
+// scene dumped by tools/wide_stack_depth.py: camera-like rays (camera
+// position to random points of random spheres) and bounce-like rays (from a
+// sphere's surface, random outward direction), walked with the kernel's
+// order (nearest hit child next, other hits pushed far first) and culling
+// (tb = nearest root so far), unbounded stack.  Prints the distribution of
+// the maximum stack depth per ray.
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "../cpu-path-tracing_amd/csrc/bvh_build.hpp"
+
+using namespace ptg;
+
+static double hit_sphere(const ptg_sphere &s, const double o[3], const double d[3])
+{
+    double e[3] = {o[0] - s.position[0], o[1] - s.position[1], o[2] - s.position[2]};
+    const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+    const double b = e[0] * d[0] + e[1] * d[1] + e[2] * d[2];
+    const double c = e[0] * e[0] + e[1] * e[1] + e[2] * e[2] - s.radius * s.radius;
+    const double disc = b * b - a * c;
+    if (disc < 0)
+        return INFINITY;
+    const double sq = std::sqrt(disc);
+    double t = (-b - sq) / a;
+    if (t < 1e-4)
+        t = (-b + sq) / a;
+    return t < 1e-4 ? INFINITY : t;
+}
+
+static bool box_hit_d(const WideGrid &g, const BvhNodeQ &q, const double o[3], const double d[3], double tb)
+{
+    const uint16_t qv[6] = {(uint16_t)(q.xy_min & 0xFFFFu), (uint16_t)(q.xy_min >> 16),
+                            (uint16_t)(q.z_min_x_max & 0xFFFFu), (uint16_t)(q.z_min_x_max >> 16),
+                            (uint16_t)(q.y_max_z_max & 0xFFFFu), (uint16_t)(q.y_max_z_max >> 16)};
+    double tin = 0, tout = tb;
+    for (int c = 0; c < 3; ++c) {
+        const double a = g.centre[c] + half_value(qv[c]) * (double)g.scale[c];
+        const double b = g.centre[c] + half_value(qv[3 + c]) * (double)g.scale[c];
+        const double t1 = (a - o[c]) / d[c], t2 = (b - o[c]) / d[c];
+        tin = std::max(tin, std::min(t1, t2));
+        tout = std::min(tout, std::max(t1, t2));
+    }
+    return tin <= tout;
+}
+
+// the kernel's float box test (ptg_render.hip box_hit_sorted; 1/d for v_rcp_f32)
+static bool box_hit_f(const WideGrid &g, const BvhNodeQ &q, const double o[3], const double d[3], double tb)
+{
+    float s[3], b[3];
+    for (int c = 0; c < 3; ++c) {
+        const float dc = (float)d[c];
+        const float ic = dc != 0.0f ? 1.0f / dc : std::copysign(1e30f, dc);
+        s[c] = g.scale[c] * ic;
+        b[c] = (g.centre[c] - (float)o[c]) * ic;
+    }
+    const uint16_t qv[6] = {(uint16_t)(q.xy_min & 0xFFFFu), (uint16_t)(q.xy_min >> 16),
+                            (uint16_t)(q.z_min_x_max & 0xFFFFu), (uint16_t)(q.z_min_x_max >> 16),
+                            (uint16_t)(q.y_max_z_max & 0xFFFFu), (uint16_t)(q.y_max_z_max >> 16)};
+    float tn[3], tf[3];
+    for (int c = 0; c < 3; ++c) {
+        tn[c] = std::fma((float)half_value(qv[c]), s[c], b[c]);
+        tf[c] = std::fma((float)half_value(qv[3 + c]), s[c], b[c]);
+    }
+    const float tcap = (float)tb * 1.0001f;
+    const float tin = std::max(std::max(tn[0], tn[1]), std::max(tn[2], 0.0f));
+    const float tout = std::min(std::min(tf[0], tf[1]), std::min(tf[2], tcap));
+    return !(tin > tout);
+}
+
+static bool g_float = false;
+
+// the kernel's scheme: a short stack of cap entries; remaining hits after the
+// nearest: one -> its word, several -> the position (node, slot of the next
+// hit); overflow -> stack cleared, resume position R (continuation chain)
+static double walk_short(const ptg_sphere *s, const BvhBuild &b, const WideGrid &g, const std::vector<BvhNodeQ> &w,
+                         const std::vector<int32_t> &cont, const double o[3], const double d[3], int cap, long &steps,
+                         long &overflows)
+{
+    double tb = INFINITY;
+    for (int i : b.big)
+        tb = std::min(tb, hit_sphere(s[i], o, d));
+    std::vector<int> st;
+    int R = -1, ni = 0;
+    for (;;) {
+        int next = -1;
+        if (ni >= 0) {
+            ++steps;
+            const int base = ni & ~3, s0 = ni & 3;
+            int hits[kWide], nh = 0;
+            for (int k = s0; k < kWide; ++k)
+                if (g_float ? box_hit_f(g, w[base + k], o, d, tb)
+                            : (w[base + k].word != kWideEmpty && box_hit_d(g, w[base + k], o, d, tb)))
+                    hits[nh++] = k;
+            if (nh >= 2) {
+                const int e = nh == 2 ? w[base + hits[1]].word : base + hits[1];
+                if ((int)st.size() == cap) {
+                    ++overflows;
+                    st.clear();
+                    R = base + hits[1];
+                } else {
+                    st.push_back(e);
+                }
+            }
+            if (nh)
+                next = w[base + hits[0]].word;
+        } else {
+            next = ni;
+        }
+        for (;;) {
+            if (next == -1) {
+                if (!st.empty()) {
+                    next = st.back();
+                    st.pop_back();
+                } else if (R != -1) {
+                    next = R;
+                    R = cont[(R & ~3) / kWide];
+                } else {
+                    break;
+                }
+            }
+            if (next < -1) {  // a leaf: test at once here
+                const int leaf = next & 0x7FFFFFFF, first = leaf & 0xFFFFFF, cnt = leaf >> 24;
+                for (int j = first; j < first + cnt; ++j)
+                    tb = std::min(tb, hit_sphere(s[b.order[j]], o, d));
+                next = -1;
+                continue;
+            }
+            break;
+        }
+        if (next == -1)
+            break;
+        ni = next;
+    }
+    return tb;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 2)
+        return 2;
+    FILE *f = std::fopen(argv[1], "rb");
+    double cam[3];
+    int n = 0;
+    if (!f || std::fread(cam, sizeof(double), 3, f) != 3 || std::fread(&n, sizeof(int), 1, f) != 1)
+        return 2;
+    std::vector<ptg_sphere> s(n);
+    if (std::fread(s.data(), sizeof(ptg_sphere), n, f) != (size_t)n)
+        return 2;
+    std::fclose(f);
+    std::vector<char> huge(n);
+    for (int i = 0; i < n; ++i)
+        huge[i] = s[i].radius >= 1000.0;
+    const BvhBuild b = build_bvh(s.data(), n, huge);
+    const WideGrid g(b.nodes[0]);
+    std::vector<std::vector<BvhNodeQ>> lay(8);
+    for (int k = 0; k < 8; ++k)
+        lay[k] = wide_bvh(b, k, 0);
+    std::printf("%d spheres, %zu binary nodes, %zu wide records\n", n, b.nodes.size(), lay[0].size());
+    std::vector<std::vector<int32_t>> cont(8);
+    for (int k = 0; k < 8; ++k) {
+        cont[k] = wide_conts(lay[k], 0);
+    }
+    const int caps[4] = {1, 2, 3, 4};
+    long ssteps[4] = {0, 0, 0, 0}, sover[4] = {0, 0, 0, 0}, mism = 0;
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    std::vector<long> hist(64, 0);
+    long steps = 0, rays = 0;
+    const int nrays = argc > 2 ? std::atoi(argv[2]) : 200000;
+    g_float = argc > 3;
+    for (int r = 0; r < nrays; ++r) {
+        double o[3], d[3];
+        const ptg_sphere &t = s[b.order[rng() % b.order.size()]];
+        double u[3];
+        double len;
+        do {
+            for (int c = 0; c < 3; ++c)
+                u[c] = 2 * U(rng) - 1;
+            len = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+        } while (len > 1 || len < 1e-3);
+        if (r & 1) {  // camera-like
+            for (int c = 0; c < 3; ++c) {
+                o[c] = cam[c];
+                d[c] = t.position[c] + t.radius * u[c] / len - cam[c];
+            }
+        } else {  // bounce-like: from the surface, outward hemisphere
+            double nrm[3], w[3];
+            do {
+                for (int c = 0; c < 3; ++c)
+                    w[c] = 2 * U(rng) - 1;
+            } while (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] > 1);
+            double dn = 0;
+            for (int c = 0; c < 3; ++c) {
+                nrm[c] = u[c] / len;
+                o[c] = t.position[c] + t.radius * nrm[c];
+                dn += w[c] * nrm[c];
+            }
+            for (int c = 0; c < 3; ++c)
+                d[c] = dn < 0 ? w[c] - 2 * dn * nrm[c] : w[c];
+        }
+        const int oct = (d[0] < 0) | ((d[1] < 0) << 1) | ((d[2] < 0) << 2);
+        const std::vector<BvhNodeQ> &w = lay[oct];
+        double tb = INFINITY;
+        for (int i : b.big)
+            tb = std::min(tb, hit_sphere(s[i], o, d));
+        std::vector<int> st;
+        int cur = 0, maxd = 0;
+        for (;;) {
+            int next = -1;
+            if (cur >= 0) {
+                ++steps;
+                std::vector<int> hits;
+                for (int k = 0; k < kWide; ++k) {
+                    const BvhNodeQ &q = w[cur + k];
+                    if (q.word == kWideEmpty)
+                        continue;
+                    if (box_hit_d(g, q, o, d, tb))
+                        hits.push_back(q.word);
+                }
+                for (int k = (int)hits.size() - 1; k >= 1; --k)
+                    st.push_back(hits[k]);
+                if (!hits.empty())
+                    next = hits[0];
+            } else {
+                next = cur;
+            }
+            maxd = std::max(maxd, (int)st.size());
+            if (next == -1) {
+                if (st.empty())
+                    break;
+                next = st.back();
+                st.pop_back();
+            }
+            while (next < -1) {  // leaf: test now
+                const int leaf = next & 0x7FFFFFFF, first = leaf & 0xFFFFFF, cnt = leaf >> 24;
+                for (int j = first; j < first + cnt; ++j)
+                    tb = std::min(tb, hit_sphere(s[b.order[j]], o, d));
+                if (st.empty()) {
+                    next = -1;
+                    break;
+                }
+                next = st.back();
+                st.pop_back();
+            }
+            if (next == -1)
+                break;
+            cur = next;
+        }
+        hist[std::min(maxd, 63)] += 1;
+        for (int c = 0; c < 4; ++c) {
+            long ov = 0;
+            const double t2 = walk_short(s.data(), b, g, w, cont[oct], o, d, caps[c], ssteps[c], ov);
+            sover[c] += ov > 0;
+            mism += !(t2 == tb);
+        }
+        ++rays;
+    }
+    std::printf("node steps per ray %.2f\nmax depth: count (cumulative fraction)\n", (double)steps / rays);
+    long cum = 0;
+    for (int k = 0; k < 64; ++k)
+        if (hist[k]) {
+            cum += hist[k];
+            std::printf("%2d: %8ld  %.6f\n", k, hist[k], (double)cum / rays);
+        }
+    for (int c = 0; c < 4; ++c)
+        std::printf("short stack %d: node steps per ray %.2f, rays overflowing %.4f\n", caps[c],
+                    (double)ssteps[c] / rays, (double)sover[c] / rays);
+    std::printf("nearest-hit mismatches vs the full walk: %ld\n", mism);
+    return 0;
+}
