@@ -91,6 +91,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_FRAC
 #define PTG_LEAF_FRAC 6  // BVH: leaf phase once 6/8 of the walking lanes hold a leaf (measured: 6 beats 4 by 2 %)
 #endif
+#ifndef PTG_LEAF_CHUNK
+#define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
+#endif
 #ifndef PTG_BVH_UNIT_MULT
 #define PTG_BVH_UNIT_MULT 2  // BVH scenes below the split-tail threshold: this many times more work units (8-way C5 shards: 2 beats 1 and 4 by 2-5 %)
 #endif
@@ -161,8 +164,20 @@ __device__ unsigned long long ptg_dbg_stats[256 * 16];
         if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                                        \
             atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + (i)], 1ull);                            \
     } while (0)
+// BVH kernel, PTG_BLOCK_STATS=2: wave cycles (s_memtime) per phase of the
+// main loop in [8..13]: scan starts, node steps, leaf phases, shading,
+// refills, loop control
+#define PTG_PHASE(i)                                                                                   \
+    do {                                                                                               \
+        if constexpr (kBvh && PTG_BLOCK_STATS == 2) {                                                  \
+            const unsigned long long t_ = clock64();                                                   \
+            ph_cyc[i] += t_ - ph_t;                                                                    \
+            ph_t = t_;                                                                                 \
+        }                                                                                              \
+    } while (0)
 #else
 #define PTG_STAT(i) ((void)0)
+#define PTG_PHASE(i) ((void)0)
 #endif
 #ifndef PTG_WAVE_STATS
 #define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
@@ -625,8 +640,9 @@ struct BvhTrav {
     int best;  // winner's scene index or -1
 #if PTG_BVH_WIDE
     // wide walk: ni = the next position (a wide node's first record + the
-    // slot to resume from, >= 0), a leaf word (< -1, parked at the next
-    // chance) or -1 (walk finished).  A two-entry stack (top first, -1 empty)
+    // slot to resume from, >= 0), -1 (walk finished), or -- only while a leaf
+    // is parked -- kPopLater (-2: pop the stack after the leaf phase) or a
+    // leaf word (parked after the leaf phase).  A two-entry stack (top first, -1 empty)
     // of positions / leaf words still to visit; when it overflows it is
     // cleared and the walk continues, once it runs dry, from the resume
     // position `res` and its continuation chain (bvh_build.hpp wide_conts:
@@ -753,49 +769,54 @@ __device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, 
 }
 
 // One wide node step at position ni (node + first slot): the node's 4
-// records (one 64-B line) in one go; the nearest hit child (slots are in
-// near-first order for the layout's octant) is visited next; one more hit
-// goes on the stack as itself, several as the position of the second (the
-// node is re-tested from there, with the culling distance of then); a hit
-// leaf is parked in tr.pend.  A leaf word from the stack is parked without a
-// load.  Selections are branch-free (v_cndmask).
+// records (one 64-B line) in one go.  Slots are in near-first order for the
+// layout's octant.  The nearest hit child is visited next -- or, when it is a
+// leaf, parked in tr.pend and the second hit visited next; of the hits after
+// that one goes on the stack as itself, several as the position of the first
+// (the node is re-tested from there, with the culling distance of then).
+// With no successor the stack is popped -- at most once per step, and not
+// when a leaf was parked: ni = kPopLater then, and the leaf phase pops.
+// Selections are branch-free (v_cndmask).
+constexpr int kPopLater = -2;
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
                                               ScanCount &cnt)
 {
-    int next = tr.ni;  // a leaf word from the stack, or -1
-    if (tr.ni >= 0) {
-        const int base = tr.ni & ~3;
-        gptr<u32x4> q = qnodes + base;
-        const u32x4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-        if constexpr (kCount)
-            cnt.boxes += 4 - (tr.ni & 3);
-        const float tcap = tr.tb * 1.0001f;
-        const unsigned m = ((box_hit_sorted(q0, r, tcap) ? 1u : 0u) | (box_hit_sorted(q1, r, tcap) ? 2u : 0u) |
-                            (box_hit_sorted(q2, r, tcap) ? 4u : 0u) | (box_hit_sorted(q3, r, tcap) ? 8u : 0u)) &
-                           (0xFu << (tr.ni & 3));
-        // the word of the lowest set bit of x (x != 0)
-        auto lowest = [&](unsigned x) {
-            int w = (int)q3.w;
-            w = (x & 4u) ? (int)q2.w : w;
-            w = (x & 2u) ? (int)q1.w : w;
-            return (x & 1u) ? (int)q0.w : w;
-        };
-        next = m != 0u ? lowest(m) : -1;
-        const unsigned rest = m & (m - 1u);
-        const int pos = base + (int)__builtin_ctz(rest | 16u);
-        const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
-        const bool push = rest != 0u, full = tr.s1 != -1;
-        tr.res = (push && full) ? pos : tr.res;
-        const int s0 = tr.s0;
-        tr.s0 = push ? (full ? -1 : e) : s0;
-        tr.s1 = push ? (full ? -1 : s0) : tr.s1;
-    }
-    if (next == -1)
+    const int base = tr.ni & ~3;
+    gptr<u32x4> q = qnodes + base;
+    const u32x4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    if constexpr (kCount)
+        cnt.boxes += 4 - (tr.ni & 3);
+    const float tcap = tr.tb * 1.0001f;
+    const unsigned m = ((box_hit_sorted(q0, r, tcap) ? 1u : 0u) | (box_hit_sorted(q1, r, tcap) ? 2u : 0u) |
+                        (box_hit_sorted(q2, r, tcap) ? 4u : 0u) | (box_hit_sorted(q3, r, tcap) ? 8u : 0u)) &
+                       (0xFu << (tr.ni & 3));
+    // the word of the lowest set bit of x (x != 0)
+    auto lowest = [&](unsigned x) {
+        int w = (int)q3.w;
+        w = (x & 4u) ? (int)q2.w : w;
+        w = (x & 2u) ? (int)q1.w : w;
+        return (x & 1u) ? (int)q0.w : w;
+    };
+    const unsigned r1 = m & (m - 1u);  // hits after the first
+    const int wf = lowest(m), ws = lowest(r1);
+    const bool leaf = m != 0u && wf < kPopLater;  // the first hit is a leaf: parked
+    const unsigned rest = leaf ? r1 & (r1 - 1u) : r1;
+    int next = m == 0u ? -1 : leaf ? (r1 != 0u ? ws : kPopLater) : wf;
+    tr.pend = leaf ? (wf & 0x7FFFFFFF) : tr.pend;
+    const int pos = base + (int)__builtin_ctz(rest | 16u);
+    const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
+    const bool push = rest != 0u, full = tr.s1 != -1;
+    tr.res = (push && full) ? pos : tr.res;
+    const int s0 = tr.s0;
+    tr.s0 = push ? (full ? -1 : e) : s0;
+    tr.s1 = push ? (full ? -1 : s0) : tr.s1;
+    if (next == -1) {
         next = bvh_pop(cont, tr);
-    if (next < -1) {
-        tr.pend = next & 0x7FFFFFFF;
-        next = bvh_pop(cont, tr);
+        if (next < kPopLater) {  // a leaf from the stack
+            tr.pend = next & 0x7FFFFFFF;
+            next = kPopLater;
+        }
     }
     tr.ni = next;
 }
@@ -823,18 +844,30 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 {
     const float a = dot3(d, d);
     const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
+#if PTG_LEAF_CHUNK > 0
+    // at most PTG_LEAF_CHUNK spheres per leaf phase; the rest stays parked
+    const int take = nl < PTG_LEAF_CHUNK ? nl : PTG_LEAF_CHUNK;
+#else
+    const int take = nl;
+#endif
     if constexpr (kCount)
-        cnt.spheres += nl;
-    for (int j = 0; j < nl; ++j) {
+        cnt.spheres += take;
+    for (int j = 0; j < take; ++j) {
         const float t = root_lex<false>(A.bvh_sph[first + j], float4{}, o, d, a, tr.tb);
         if (t <= tr.tb)  // the scene index is read only for a candidate that wins or ties
             update_lex(t, A.bvh_id[first + j], tr.tb, tr.best);
     }
-    tr.pend = -1;
+    tr.pend = take < nl ? ((first + take) | ((nl - take) << 24)) : -1;
+    if (tr.pend >= 0)
+        return;
 #if PTG_BVH_WIDE
-    if (tr.ni < -1) {
-        tr.pend = tr.ni & 0x7FFFFFFF;
-        tr.ni = bvh_pop(cont, tr);
+    if (tr.ni < -1) {  // kPopLater, or the leaf the node step moved to after parking one
+        int next = tr.ni == kPopLater ? bvh_pop(cont, tr) : tr.ni;
+        if (next < kPopLater) {  // a leaf: parked for the next leaf phase
+            tr.pend = next & 0x7FFFFFFF;
+            next = kPopLater;
+        }
+        tr.ni = next;
     }
 #else
     (void)cont;
@@ -1281,15 +1314,20 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         asm volatile("" : "+s"(trig));
         int oct_mask = A.bvh_oct_mask;
         asm volatile("" : "+s"(oct_mask));
+#if PTG_BLOCK_STATS == 2
+        unsigned long long ph_cyc[6] = {0, 0, 0, 0, 0, 0}, ph_t = clock64();
+#endif
         for (;;) {
             if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
                 break;
+            PTG_PHASE(5);
             if (item >= 0 && phase == 0) {
                 if constexpr (kCount)
                     segs += 1;
                 bvh_start<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt, oct_mask);
                 phase = bvh_done(A, tr) ? 2 : 1;
             }
+            PTG_PHASE(0);
             {
                 const SlabRay sr = slab_ray(A, o, d);
                 for (;;) {
@@ -1321,8 +1359,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         // tests are cheap next to the node steps' memory latency)
                         if (trv && tr.pend >= 0)
                             bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
-                    } else if (trv && tr.pend < 0) {  // node step
-                        bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
+                        PTG_PHASE(2);
+                    } else {
+                        PTG_PHASE(5);
+                        if (trv && tr.pend < 0)  // node step
+                            bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
+                        PTG_PHASE(1);
                     }
                     if (trv && bvh_done(A, tr))
                         phase = 2;
@@ -1335,13 +1377,21 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 scnt.spheres += (first_lane && __ballot(item >= 0 && phase == 2) != 0ull) ? 1 : 0;
             }
 #endif
+            PTG_PHASE(5);
             if (item >= 0 && phase == 2) {
                 phase = 0;
                 if (shade(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
+            PTG_PHASE(3);
             refill();
+            PTG_PHASE(4);
         }
+#if PTG_BLOCK_STATS == 2
+        if (lane == 0)
+            for (int k = 0; k < 6; ++k)
+                atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + 8 + k], ph_cyc[k]);
+#endif
     }
     if (parked)
         flush_parked();

@@ -1,0 +1,37 @@
+"""Wave cycles per phase of the BVH kernel's main loop (debug build:
+make -C cpu-path-tracing_amd variant NAME=phase DEFS=-DPTG_BLOCK_STATS=2), on
+C5's scene at 1920x1080 with 16 spp.  Run on the GPU box:
+python tools/phase_times.py [variant ...]"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) == 1 or sys.argv[1] != "--one":
+    for v in sys.argv[1:] or ("phase",):
+        env = dict(os.environ, PTGPU_LIB=os.path.join(ROOT, "cpu-path-tracing_amd", "build", f"libptgpu_{v}.so"))
+        subprocess.check_call([sys.executable, __file__, "--one", v], env=env)
+    sys.exit(0)
+sys.path.insert(0, os.path.join(ROOT, "cpu-path-tracing_amd"))
+import torch  # noqa: E402
+
+import ptgpu  # noqa: E402
+
+NAMES = ["scan_start", "node_steps", "leaf_phases", "shade", "refill", "loop_control"]
+W, H, samps = 1920, 1080, 16
+scn = ptgpu.make_scene("synthetic:10000", W, H)
+cam = ptgpu.camera.with_config(scn.camera_parameters)
+out = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+segs = torch.zeros(1, dtype=torch.int64, device="cuda")
+st = (C.c_ulonglong * 16)()
+ptgpu.lib().ptg_debug_stats_(st)  # zero
+with ptgpu.Context(scn, cam) as ctx:
+    ctx.render_device(out, ptgpu.make_params(W, H, samps), segs)
+    torch.cuda.synchronize()
+ptgpu.lib().ptg_debug_stats_(st)
+cyc = [st[8 + k] for k in range(6)]
+tot = sum(cyc)
+lane_segs = int(segs.item())
+print(sys.argv[2], "wave cycles per 64 lane-segments:",
+      " ".join(f"{n} {64 * c / lane_segs:.0f} ({100 * c / tot:.1f} %)" for n, c in zip(NAMES, cyc)))
