@@ -91,6 +91,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_FRAC
 #define PTG_LEAF_FRAC 6  // BVH: leaf phase once 6/8 of the walking lanes hold a leaf (measured: 6 beats 4 by 2 %)
 #endif
+#ifndef PTG_LEAF_SPLIT
+#define PTG_LEAF_SPLIT 1  // BVH leaf phase: lanes without a leaf test the second half of another lane's leaf
+#endif
 #ifndef PTG_LEAF_CHUNK
 #define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
 #endif
@@ -837,29 +840,27 @@ __device__ __forceinline__ void bvh_node_step(gptr<int>, gptr<u32x4> qnodes, con
 }
 #endif
 
-// The parked leaf's spheres: compact records {C, -R^2} in leaf order.  Wide
-// walk: a leaf word waiting in tr.ni is parked next.
+// Spheres [f, f + cnt) of the leaf order against one ray: compact records
+// {C, -R^2}; (tb, best) updated by the lex rule.
 template <bool kCount>
-__device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
+__device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 o, f3 d, float &tb, int &best,
+                                             ScanCount &sc)
 {
     const float a = dot3(d, d);
-    const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
-#if PTG_LEAF_CHUNK > 0
-    // at most PTG_LEAF_CHUNK spheres per leaf phase; the rest stays parked
-    const int take = nl < PTG_LEAF_CHUNK ? nl : PTG_LEAF_CHUNK;
-#else
-    const int take = nl;
-#endif
     if constexpr (kCount)
-        cnt.spheres += take;
-    for (int j = 0; j < take; ++j) {
-        const float t = root_lex<false>(A.bvh_sph[first + j], float4{}, o, d, a, tr.tb);
-        if (t <= tr.tb)  // the scene index is read only for a candidate that wins or ties
-            update_lex(t, A.bvh_id[first + j], tr.tb, tr.best);
+        sc.spheres += cnt;
+    for (int j = 0; j < cnt; ++j) {
+        const float t = root_lex<false>(A.bvh_sph[f + j], float4{}, o, d, a, tb);
+        if (t <= tb)  // the scene index is read only for a candidate that wins or ties
+            update_lex(t, A.bvh_id[f + j], tb, best);
     }
-    tr.pend = take < nl ? ((first + take) | ((nl - take) << 24)) : -1;
-    if (tr.pend >= 0)
-        return;
+}
+
+// After the parked leaf's spheres: wide walk -- a leaf word waiting in tr.ni
+// is parked next, or the pop deferred by the node step happens.
+__device__ __forceinline__ void bvh_leaf_done(gptr<int> cont, BvhTrav &tr)
+{
+    tr.pend = -1;
 #if PTG_BVH_WIDE
     if (tr.ni < -1) {  // kPopLater, or the leaf the node step moved to after parking one
         int next = tr.ni == kPopLater ? bvh_pop(cont, tr) : tr.ni;
@@ -872,6 +873,96 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 #else
     (void)cont;
 #endif
+}
+
+// The parked leaf's spheres, all by this lane.
+template <bool kCount>
+__device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
+{
+    const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
+#if PTG_LEAF_CHUNK > 0
+    // at most PTG_LEAF_CHUNK spheres per leaf phase; the rest stays parked
+    const int take = nl < PTG_LEAF_CHUNK ? nl : PTG_LEAF_CHUNK;
+#else
+    const int take = nl;
+#endif
+    leaf_spheres<kCount>(A, first, take, o, d, tr.tb, tr.best, cnt);
+    if (take < nl) {
+        tr.pend = (first + take) | ((nl - take) << 24);
+        return;
+    }
+    bvh_leaf_done(cont, tr);
+}
+
+// Leaf phase with helpers (PTG_LEAF_SPLIT; called by the whole wave): lanes
+// with no leaf to test are paired, by rank, with lanes holding a leaf of >= 2
+// spheres; the helper takes the leaf's second half with the owner's ray and
+// culling distance (ds_bpermute), and the owner merges the helper's nearest
+// root by the same lex rule -- which is order-independent, so the result is
+// the one-lane result bit for bit.  The wave's loop then runs about half the
+// iterations.  pair: 2 x 64 bytes of LDS (owner / helper lane of each rank).
+template <bool kCount>
+__device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f3 o, f3 d, bool has, BvhTrav &tr,
+                                               ScanCount &cnt, uint8_t (*pair)[64])
+{
+    const int lane = (int)__lane_id();
+    const int nl = has ? (tr.pend >> 24) : 0;
+    const bool own = nl >= 2, hlp = !has;
+    // owners of the longest leaves (>= 4 spheres: they set the wave's loop
+    // length) rank first, so they get the helpers when there are too few
+    auto rank = [](unsigned long long m) {
+        return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    };
+    const bool longl = nl >= 4;
+    const unsigned long long ml = __ballot(longl), ms = __ballot(own && !longl), mh = __ballot(hlp);
+    const int nlong = (int)__popcll(ml);
+    const int np = min(nlong + (int)__popcll(ms), (int)__popcll(mh));
+    const int ro = longl ? rank(ml) : nlong + rank(ms);
+    const int rh = rank(mh);
+    const bool po = own && ro < np, ph = hlp && rh < np;
+    if (po)
+        pair[0][ro] = (uint8_t)lane;
+    if (ph)
+        pair[1][rh] = (uint8_t)lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int partner = po ? (int)pair[1][ro] : ph ? (int)pair[0][rh] : lane;
+    auto bpf = [&](float v) {
+        return __int_as_float(__builtin_amdgcn_ds_bpermute(partner << 2, __float_as_int(v)));
+    };
+    auto bpi = [&](int v) { return __builtin_amdgcn_ds_bpermute(partner << 2, v); };
+    // helpers take the owner's ray, culling distance and leaf
+    const f3 po3 = mk3(bpf(o.x), bpf(o.y), bpf(o.z)), pd3 = mk3(bpf(d.x), bpf(d.y), bpf(d.z));
+    const float ptb = bpf(tr.tb);
+    const int ppend = bpi(tr.pend);
+    const f3 ro3 = ph ? po3 : o, rd3 = ph ? pd3 : d;
+    const int pendl = ph ? ppend : tr.pend;
+    const int first = pendl & 0xFFFFFF, nll = pendl >> 24, half = (nll + 1) >> 1;
+    const int f = ph ? first + half : first;
+    const int c = ph ? nll - half : po ? half : has ? nll : 0;
+    float tb = ph ? ptb : tr.tb;
+    int best = ph ? -1 : tr.best;
+#if PTG_WAVE_STATS == 1  // debug: the wave's loop length, and pairs (sphere counter's high half)
+    {
+        int mx = c;
+        for (int off = 32; off > 0; off >>= 1)
+            mx = max(mx, __shfl_xor(mx, off, 64));
+        const bool first_lane = lane == __ffsll((long long)__ballot(1)) - 1;
+        cnt.spheres += first_lane ? (uint32_t)mx : 0u;
+    }
+#endif
+    leaf_spheres<kCount && !PTG_WAVE_STATS>(A, f, c, ro3, rd3, tb, best, cnt);
+    // owners merge their helper's nearest root
+    const float htb = bpf(tb);
+    const int hbest = bpi(best);
+    if (po)
+        update_lex(htb, hbest, tb, best);
+    if (has) {
+        tr.tb = tb;
+        tr.best = best;
+        bvh_leaf_done(cont, tr);
+    }
 }
 
 // Whole scan of one ray (parity probe kernel): walk, testing each parked leaf
@@ -1304,6 +1395,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
         // of the active lanes) or none walks, shades the ready lanes.
         BvhTrav tr{};  // started per segment by bvh_start
+#if PTG_LEAF_SPLIT
+        __shared__ uint8_t lds_pair[kWaves][2][64];  // leaf phase: owner / helper lane of each rank
+#endif
         // kernel-argument pointers used in the loops, pinned in SGPRs once:
         // left to the compiler they were re-loaded (s_load + wait) in every
         // node step and every shade
@@ -1344,7 +1438,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     if constexpr (kCount) {
                         const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
                         if (8 * nh >= PTG_LEAF_FRAC * nt) {
-                            int mx = trv && tr.pend >= 0 ? (tr.pend >> 24) : 0;
+                            int mx = trv && tr.pend >= 0 && !PTG_LEAF_SPLIT ? (tr.pend >> 24) : 0;  // split: counted there
                             for (int off = 32; off > 0; off >>= 1)
                                 mx = max(mx, __shfl_xor(mx, off, 64));
                             scnt.spheres += first_lane ? mx : 0;
@@ -1354,11 +1448,16 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     }
 #endif
                     if (8 * nh >= PTG_LEAF_FRAC * nt) {  // leaf phase
-                        // (spreading the parked leaves' spheres over the whole wave with
-                        // ds_bpermute + LDS atomicMin measured 1.7 % slower: the leaf
-                        // tests are cheap next to the node steps' memory latency)
+                        // (round 1: spreading the parked leaves' spheres over the whole wave
+                        // with ds_bpermute + LDS atomicMin measured 1.7 % slower; pairing
+                        // idle lanes with the long leaves, below, 1.2-1.5 % faster)
+#if PTG_LEAF_SPLIT
+                        bvh_leaf_split<kCount && !PTG_WAVE_STATS>(A, cont, o, d, trv && tr.pend >= 0, tr, scnt,
+                                                                   lds_pair[wv]);
+#else
                         if (trv && tr.pend >= 0)
                             bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
+#endif
                         PTG_PHASE(2);
                     } else {
                         PTG_PHASE(5);
