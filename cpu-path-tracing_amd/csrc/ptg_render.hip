@@ -94,6 +94,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_SPLIT
 #define PTG_LEAF_SPLIT 1  // BVH leaf phase: lanes without a leaf test the second half of another lane's leaf
 #endif
+#ifndef PTG_SLAB_PER_STEP
+#define PTG_SLAB_PER_STEP 0  // BVH: the ray's slab constants recomputed per node step instead of held across the walk
+#endif
 #ifndef PTG_LEAF_CHUNK
 #define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
 #endif
@@ -1246,19 +1249,34 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     // the camera code runs only in refills of >= PTG_REFILL_BATCH lanes (or
     // when a lane would otherwise idle).
     __shared__ float4 lds_pre[kWaves][64][2];
+    // it / nv and it % nv (it < 2^24, only for a unit of fewer than 64
+    // slots) through a float reciprocal formed at each use: the compiler's
+    // integer division by the unit's nv kept its constants in VGPRs for the
+    // whole unit (spilled to scratch)
+    auto divmod_nv = [&](int it, int &q, int &r) {
+        int n = nv;
+        asm volatile("" : "+s"(n));
+        q = (int)((float)it * __builtin_amdgcn_rcpf((float)n));
+        r = it - q * n;
+        q = r < 0 ? q - 1 : (r >= n ? q + 1 : q);
+        r = r < 0 ? r + n : (r >= n ? r - n : r);
+    };
     auto ray_of = [&](int it, f3 &ro, f3 &rd, uint32_t &rs) {
         int sl, sample;
         if (nv == 64) {
             sl = it & 63;
             sample = s0 + (it >> 6);
         } else {
-            sl = it % nv;
-            sample = s0 + it / nv;
+            int q;
+            divmod_nv(it, q, sl);
+            sample = s0 + q;
         }
         Lane L;
         uint32_t pk = lds_pix[wv][sl];
         L.x = (int)(pk & 0xFFFFFu);
-        L.y = y;
+        int yy = y;  // opaque: (float)y is converted here, not held in a VGPR for the unit
+        asm volatile("" : "+s"(yy));
+        L.y = yy;
         L.sx = (int)((pk >> 20) & 63u);
         L.sy = (int)(pk >> 26);
         L.key = lds_key[wv][sl];
@@ -1273,7 +1291,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     auto begin = [&](int it, f3 ro, f3 rd, uint32_t rs) {
         item = it;
         phase = 0;
-        slot = nv == 64 ? (it & 63) : it % nv;
+        if (nv == 64) {
+            slot = it & 63;
+        } else {
+            int q;
+            divmod_nv(it, q, slot);
+        }
         o = ro;
         d = rd;
         st = rs;
@@ -1355,7 +1378,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     park();
                 waiting = false;
                 if (!has_pre) {
-                    const int ni = next + (int)__popcll(need & ((1ull << lane) - 1ull));
+                    // lanes of need below this one (v_mbcnt: no 64-bit lane mask held in VGPRs)
+                    const int ni = next + (int)__builtin_amdgcn_mbcnt_hi(
+                                              (unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
                     if (ni < total) {
                         f3 ro, rd;
                         uint32_t rs;
@@ -1405,9 +1430,15 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         asm volatile("" : "+s"(qnodes));
         gptr<int> cont = (gptr<int>)A.bvh_cont;
         asm volatile("" : "+s"(cont));
+#if !PTG_NO_TRIG_PIN
         asm volatile("" : "+s"(trig));
+#endif
+#if PTG_BVH_WIDE
+        const int oct_mask = 7;  // every octant has its layout
+#else
         int oct_mask = A.bvh_oct_mask;
         asm volatile("" : "+s"(oct_mask));
+#endif
 #if PTG_BLOCK_STATS == 2
         unsigned long long ph_cyc[6] = {0, 0, 0, 0, 0, 0}, ph_t = clock64();
 #endif
@@ -1423,7 +1454,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             }
             PTG_PHASE(0);
             {
+#if !PTG_SLAB_PER_STEP
                 const SlabRay sr = slab_ray(A, o, d);
+#endif
                 for (;;) {
                     const bool trv = item >= 0 && phase == 1;
                     const unsigned long long mt = __ballot(trv);
@@ -1461,8 +1494,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         PTG_PHASE(2);
                     } else {
                         PTG_PHASE(5);
-                        if (trv && tr.pend < 0)  // node step
+                        if (trv && tr.pend < 0) {  // node step
+#if PTG_SLAB_PER_STEP
+                            const SlabRay sr = slab_ray(A, o, d);  // recomputed: 6 VGPRs fewer across the walk
+#endif
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
+                        }
                         PTG_PHASE(1);
                     }
                     if (trv && bvh_done(A, tr))
@@ -1556,8 +1593,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         }
     } else if (lane < nv) {
         // several units share these pixels: exact u64 adds, resolved later
-        unsigned long long *g = A.acc + (((size_t)slab_row * A.W + x0) * A.lanes_per_pixel + lane) * 3;
-        unsigned long long vx = lds_acc[wv][lane], vy = lds_acc[wv][lane + 64], vz = lds_acc[wv][lane + 128];
+        // opaque: the address is formed here, not held in VGPRs for the unit
+        int ln = lane, row = slab_row, px0 = x0;
+        asm volatile("" : "+v"(ln), "+s"(row), "+s"(px0));
+        unsigned long long *g = A.acc + (((size_t)row * A.W + px0) * A.lanes_per_pixel + ln) * 3;
+        unsigned long long vx = lds_acc[wv][ln], vy = lds_acc[wv][ln + 64], vz = lds_acc[wv][ln + 128];
         if (vx) atomicAdd(g + 0, vx);
         if (vy) atomicAdd(g + 1, vy);
         if (vz) atomicAdd(g + 2, vz);
