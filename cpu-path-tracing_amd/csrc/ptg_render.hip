@@ -89,7 +89,7 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #define PTG_REFILL_BATCH 40  // measured: 40 beats 32 by 0.35 % (box) / 0.6 % (box_mirror), ties 48-56; 24 is 1.2 % slower
 #endif
 #ifndef PTG_LEAF_FRAC
-#define PTG_LEAF_FRAC 6  // BVH: leaf phase once 6/8 of the walking lanes hold a leaf (measured: 6 beats 4 by 2 %)
+#define PTG_LEAF_FRAC 5  // BVH: leaf phase once 5/8 of the walking lanes hold a leaf (wide walk + leaf pairing: 5 beats 6 by 0.9 %, 7 by 3 %)
 #endif
 #ifndef PTG_LEAF_SPLIT
 #define PTG_LEAF_SPLIT 1  // BVH leaf phase: lanes without a leaf test the second half of another lane's leaf
