@@ -80,6 +80,24 @@ def test_image_bitexact_vs_oracle(name, W, H, samps):
         assert 0 < ntest < nseg * n / 5 and nbox > 0
 
 
+def test_wide_bvh_overflow_scene_bitexact():
+    """An overlap-heavy cluster (tests/wide_scenes.py): 87 % of the rays
+    overflow the wide walk's two-entry stack (tools/wide_stack_depth.cpp), so
+    the continuation fallback runs constantly; the image stays bit-exact with
+    the oracle's linear scan."""
+    _require_gpu()
+    from wide_scenes import cluster_scene
+    W, H, samps = 48, 27, 4
+    scn = cluster_scene(1500, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    gpu, gsegs = _gpu_image(scn, cam, W, H, samps, count_segments=True)
+    sp, ca = _oracle_scene(scn, cam)
+    ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
+    _check_equal(gpu, ref)
+    assert gsegs == rsegs
+    assert float(ref.mean()) > 0.01  # the cluster is in view and lit
+
+
 @pytest.mark.parametrize("order", [[5, 6, 7, 0, 1, 2, 3, 4], [0, 5, 1, 6, 2, 7, 3, 4], [7, 6, 5, 4, 3, 2, 1, 0]])
 def test_sphere_order_layouts(order):
     """The host regroups the records into scan order (axis-anchored walls by
