@@ -173,14 +173,18 @@ __device__ unsigned long long ptg_dbg_stats[256 * 16];
 // BVH kernel, PTG_BLOCK_STATS=2: wave cycles (s_memtime) per phase of the
 // main loop in [8..13]: scan starts, node steps, leaf phases, shading,
 // refills, loop control
+#if PTG_BLOCK_STATS == 2
 #define PTG_PHASE(i)                                                                                   \
     do {                                                                                               \
-        if constexpr (kBvh && PTG_BLOCK_STATS == 2) {                                                  \
+        if constexpr (kBvh) {                                                                          \
             const unsigned long long t_ = clock64();                                                   \
             ph_cyc[i] += t_ - ph_t;                                                                    \
             ph_t = t_;                                                                                 \
         }                                                                                              \
     } while (0)
+#else
+#define PTG_PHASE(i) ((void)0)
+#endif
 #else
 #define PTG_STAT(i) ((void)0)
 #define PTG_PHASE(i) ((void)0)
@@ -1401,10 +1405,34 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         }
     };
     if constexpr (!kBvh) {
+#if PTG_BLOCK_STATS == 3  // debug: wave cycles of the linear kernel's scan / shade / refill / loop control
+        unsigned long long ph_cyc[6] = {0, 0, 0, 0, 0, 0}, ph_t = clock64();
+        auto lin_phase = [&](int i) {
+            const unsigned long long t_ = clock64();
+            ph_cyc[i] += t_ - ph_t;
+            ph_t = t_;
+        };
+#endif
         for (;;) {
             if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
                 break;
             PTG_STAT(0);
+#if PTG_BLOCK_STATS == 3
+            lin_phase(5);
+            float t3 = 0.0f;
+            const LinRec *w3 = nullptr;
+            if (item >= 0) {
+                if constexpr (kCount)
+                    segs += 1;
+                w3 = scene_scan(A, recs, o, d, t3);
+            }
+            lin_phase(0);
+            if (item >= 0 && shade(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st))
+                path_done();
+            lin_phase(3);
+            refill();
+            lin_phase(4);
+#else
             if (item >= 0) {
                 PTG_STAT(1);
                 if constexpr (kCount)
@@ -1413,7 +1441,13 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     path_done();
             }
             refill();
+#endif
         }
+#if PTG_BLOCK_STATS == 3
+        if (lane == 0)
+            for (int k = 0; k < 6; ++k)
+                atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + 8 + k], ph_cyc[k]);
+#endif
     } else {
         // BVH scenes: each lane is fresh (ray set, scan not started), walking
         // or ready (scan done, to be shaded); an iteration starts the fresh

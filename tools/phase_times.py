@@ -20,7 +20,10 @@ import ptgpu  # noqa: E402
 
 NAMES = ["scan_start", "node_steps", "leaf_phases", "shade", "refill", "loop_control"]
 W, H, samps = 1920, 1080, 16
-scn = ptgpu.make_scene("synthetic:10000", W, H)
+scene = os.environ.get("PHASE_SCENE", "synthetic:10000")  # a linear scene needs PTG_BLOCK_STATS=3 (scan in slot 0)
+if not scene.startswith("synthetic"):
+    NAMES[0] = "scan"
+scn = ptgpu.make_scene(scene, W, H)
 cam = ptgpu.camera.with_config(scn.camera_parameters)
 out = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
 segs = torch.zeros(1, dtype=torch.int64, device="cuda")
