@@ -92,7 +92,7 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #define PTG_LEAF_FRAC 5  // BVH: leaf phase once 5/8 of the walking lanes hold a leaf (wide walk + leaf pairing: 5 beats 6 by 0.9 %, 7 by 3 %)
 #endif
 #ifndef PTG_LEAF_SPLIT
-#define PTG_LEAF_SPLIT 1  // BVH leaf phase: lanes without a leaf test the second half of another lane's leaf
+#define PTG_LEAF_SPLIT 2  // BVH leaf phase: lanes without a leaf test part of another lane's leaf (1: one helper per leaf, 2: up to two)
 #endif
 #ifndef PTG_SLAB_PER_STEP
 #define PTG_SLAB_PER_STEP 0  // BVH: the ray's slab constants recomputed per node step instead of held across the walk
@@ -902,12 +902,14 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 }
 
 // Leaf phase with helpers (PTG_LEAF_SPLIT; called by the whole wave): lanes
-// with no leaf to test are paired, by rank, with lanes holding a leaf of >= 2
-// spheres; the helper takes the leaf's second half with the owner's ray and
-// culling distance (ds_bpermute), and the owner merges the helper's nearest
-// root by the same lex rule -- which is order-independent, so the result is
-// the one-lane result bit for bit.  The wave's loop then runs about half the
-// iterations.  pair: 2 x 64 bytes of LDS (owner / helper lane of each rank).
+// with no leaf to test are assigned, by rank, to lanes holding a leaf of >= 2
+// spheres -- one helper per such leaf, longest leaves (>= 4 spheres: they set
+// the wave's loop length) first, then a second helper per long leaf while
+// idle lanes remain.  A helper tests its part of the leaf with the owner's
+// ray and culling distance (ds_bpermute) and the owner merges the helpers'
+// nearest roots by the same lex rule -- order-independent, so the result is
+// the one-lane result bit for bit.  pair: 2 x 64 bytes of LDS (owner lane by
+// owner rank, helper lane by helper rank).
 template <bool kCount>
 __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f3 o, f3 d, bool has, BvhTrav &tr,
                                                ScanCount &cnt, uint8_t (*pair)[64])
@@ -915,18 +917,21 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     const int lane = (int)__lane_id();
     const int nl = has ? (tr.pend >> 24) : 0;
     const bool own = nl >= 2, hlp = !has;
-    // owners of the longest leaves (>= 4 spheres: they set the wave's loop
-    // length) rank first, so they get the helpers when there are too few
     auto rank = [](unsigned long long m) {
         return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
     };
     const bool longl = nl >= 4;
     const unsigned long long ml = __ballot(longl), ms = __ballot(own && !longl), mh = __ballot(hlp);
-    const int nlong = (int)__popcll(ml);
-    const int np = min(nlong + (int)__popcll(ms), (int)__popcll(mh));
+    const int nlong = (int)__popcll(ml), nown = nlong + (int)__popcll(ms), nhelp = (int)__popcll(mh);
+    const int np1 = min(nown, nhelp);  // owners (by rank) with a first helper
+#if PTG_LEAF_SPLIT >= 2
+    const int np2 = max(0, min(nlong, nhelp - nown));  // long-leaf owners with a second helper
+#else
+    const int np2 = 0;
+#endif
     const int ro = longl ? rank(ml) : nlong + rank(ms);
     const int rh = rank(mh);
-    const bool po = own && ro < np, ph = hlp && rh < np;
+    const bool po = own && ro < np1, ph = hlp && rh < np1 + np2;
     if (po)
         pair[0][ro] = (uint8_t)lane;
     if (ph)
@@ -934,23 +939,33 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int partner = po ? (int)pair[1][ro] : ph ? (int)pair[0][rh] : lane;
-    auto bpf = [&](float v) {
-        return __int_as_float(__builtin_amdgcn_ds_bpermute(partner << 2, __float_as_int(v)));
+    const int orank = rh < np1 ? rh : rh - np1;  // a helper's owner, and which helper it is
+    const int part = rh < np1 ? 1 : 2;
+    const int partner = po ? (int)pair[1][ro] : ph ? (int)pair[0][orank] : lane;
+    const int partner2 = (po && ro < np2) ? (int)pair[1][np1 + ro] : lane;
+    auto bpf = [](int who, float v) {
+        return __int_as_float(__builtin_amdgcn_ds_bpermute(who << 2, __float_as_int(v)));
     };
-    auto bpi = [&](int v) { return __builtin_amdgcn_ds_bpermute(partner << 2, v); };
+    auto bpi = [](int who, int v) { return __builtin_amdgcn_ds_bpermute(who << 2, v); };
     // helpers take the owner's ray, culling distance and leaf
-    const f3 po3 = mk3(bpf(o.x), bpf(o.y), bpf(o.z)), pd3 = mk3(bpf(d.x), bpf(d.y), bpf(d.z));
-    const float ptb = bpf(tr.tb);
-    const int ppend = bpi(tr.pend);
+    const f3 po3 = mk3(bpf(partner, o.x), bpf(partner, o.y), bpf(partner, o.z));
+    const f3 pd3 = mk3(bpf(partner, d.x), bpf(partner, d.y), bpf(partner, d.z));
+    const float ptb = bpf(partner, tr.tb);
+    const int ppend = bpi(partner, tr.pend);
     const f3 ro3 = ph ? po3 : o, rd3 = ph ? pd3 : d;
     const int pendl = ph ? ppend : tr.pend;
-    const int first = pendl & 0xFFFFFF, nll = pendl >> 24, half = (nll + 1) >> 1;
-    const int f = ph ? first + half : first;
-    const int c = ph ? nll - half : po ? half : has ? nll : 0;
+    const int first = pendl & 0xFFFFFF, nll = pendl >> 24;
+    // the leaf's parts: one helper -> [0, ceil(n/2)), [ceil(n/2), n); two
+    // helpers -> [0, n/3), [n/3, 2n/3), [2n/3, n) (n <= 12: x/3 = x*11 >> 5)
+    const int k = ph ? 1 + (orank < np2) : po ? 1 + (ro < np2) : 0;
+    const int b1 = k == 2 ? (nll * 11) >> 5 : (nll + 1) >> 1;
+    const int b2 = k == 2 ? (2 * nll * 11) >> 5 : nll;
+    const int lo = !ph ? 0 : part == 1 ? b1 : b2;
+    const int hi = !ph ? (po ? b1 : (has ? nll : 0)) : part == 1 ? b2 : nll;
+    const int f = first + lo, c = hi - lo;
     float tb = ph ? ptb : tr.tb;
     int best = ph ? -1 : tr.best;
-#if PTG_WAVE_STATS == 1  // debug: the wave's loop length, and pairs (sphere counter's high half)
+#if PTG_WAVE_STATS == 1  // debug: the wave's loop length
     {
         int mx = c;
         for (int off = 32; off > 0; off >>= 1)
@@ -960,11 +975,13 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     }
 #endif
     leaf_spheres<kCount && !PTG_WAVE_STATS>(A, f, c, ro3, rd3, tb, best, cnt);
-    // owners merge their helper's nearest root
-    const float htb = bpf(tb);
-    const int hbest = bpi(best);
-    if (po)
+    // owners merge their helpers' nearest roots
+    const float htb = bpf(partner, tb), htb2 = bpf(partner2, tb);
+    const int hbest = bpi(partner, best), hbest2 = bpi(partner2, best);
+    if (po) {
         update_lex(htb, hbest, tb, best);
+        update_lex(htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
+    }
     if (has) {
         tr.tb = tb;
         tr.best = best;
