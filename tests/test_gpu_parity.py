@@ -98,6 +98,25 @@ def test_wide_bvh_overflow_scene_bitexact():
     assert float(ref.mean()) > 0.01  # the cluster is in view and lit
 
 
+@pytest.mark.parametrize("n_small", [0, 1, 4])
+def test_wide_bvh_empty_and_one_leaf_trees(n_small):
+    """> 64 spheres, nearly all huge: the BVH path with an empty tree (every
+    sphere tested linearly) or a tree that is a single leaf (one wide node
+    with one child and three empty slots) -- bit-exact with the oracle."""
+    _require_gpu()
+    from wide_scenes import huge_only_scene
+    W, H, samps = 40, 30, 4
+    scn = huge_only_scene(70, n_small, W, H)
+    assert len(scn.spheres) > 64
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    gpu, gsegs = _gpu_image(scn, cam, W, H, samps, count_segments=True)
+    sp, ca = _oracle_scene(scn, cam)
+    ref, rsegs = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
+    _check_equal(gpu, ref)
+    assert gsegs == rsegs
+    assert float(ref.mean()) > 0.0
+
+
 @pytest.mark.parametrize("order", [[5, 6, 7, 0, 1, 2, 3, 4], [0, 5, 1, 6, 2, 7, 3, 4], [7, 6, 5, 4, 3, 2, 1, 0]])
 def test_sphere_order_layouts(order):
     """The host regroups the records into scan order (axis-anchored walls by

@@ -38,3 +38,30 @@ def dump_scene(scn, path: str) -> None:
         f.write(np.asarray(cam.position, np.float64).tobytes())
         f.write(np.int32(len(sp)).tobytes())
         f.write(sp.tobytes())
+
+
+def huge_only_scene(n_huge: int, n_small: int, w: int, h: int, seed: int = 11) -> "ptgpu.scene":
+    """More than 64 spheres of which at most a few are small: the BVH path
+    with an empty tree (n_small = 0) or a one-leaf tree (n_small <= 6) under
+    many huge (anchored, linearly tested) spheres."""
+    rng = np.random.default_rng(seed)
+    D, S = ptgpu.reflection_type.diffuse, ptgpu.reflection_type.specular
+    scn = ptgpu.scene([ptgpu.sphere(1.0, (0.0, 6.0, 0.0), (12.0, 12.0, 12.0), (0.8, 0.8, 0.8), D)] if n_small else [])
+    for k in range(n_huge):
+        R = float(rng.uniform(1000.0, 3000.0))
+        ang = 2.0 * np.pi * k / n_huge
+        dist = R + float(rng.uniform(8.0, 30.0))
+        pos = (dist * float(np.cos(ang)), float(rng.uniform(-20.0, 20.0)), dist * float(np.sin(ang)))
+        col = tuple(float(c) for c in rng.uniform(0.2, 0.95, 3))
+        emit = (0.3, 0.3, 0.3) if k % 9 == 0 else (0.0, 0.0, 0.0)
+        scn.spheres.append(ptgpu.sphere(R, pos, emit, col, S if k % 5 == 0 else D))
+    for k in range(max(0, n_small - 1)):
+        scn.spheres.append(ptgpu.sphere(0.5 + 0.2 * k, (1.5 * k - 2.0, 0.5, 0.0), (0.0, 0.0, 0.0), (0.7, 0.3, 0.3), D))
+    c = scn.camera_parameters
+    c.position = (0.0, 2.0, 6.0)
+    c.direction = (0.0, 1.0, 0.0)
+    c.aspect_ratio = w / h
+    c.vertical_fov_radians = 1.2
+    c.aperture = 0.0
+    c.focus_distance = ptgpu.length((0.0, 1.0, 6.0))
+    return scn
