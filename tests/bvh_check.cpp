@@ -135,6 +135,10 @@ static void wide_walk(const std::vector<ptg_sphere> &s, const BvhBuild &b, const
 
 static void check_wide(const std::vector<ptg_sphere> &s, const BvhBuild &b)
 {
+    if (b.nodes.empty()) {  // every sphere huge: no tree, no wide layout
+        CHECK(wide_bvh(b, 0, 0).empty() && wide_conts(wide_bvh(b, 0, 0), 0).empty(), "empty tree: wide layout");
+        return;
+    }
     const WideGrid g(b.nodes[0]);
     for (int oct = 0; oct < 8 && !fails; ++oct) {
         const int32_t base = 1000 * oct;
@@ -198,6 +202,12 @@ static void check_scene(const std::vector<ptg_sphere> &s)
     }
     const int nn = (int)b.nodes.size();
     CHECK((int)b.axis.size() == nn, "axis per node");
+    if (nn == 0) {
+        check_wide(s, b);
+        if (!fails)
+            std::printf("ok %d spheres, all huge: empty tree\n", n);
+        return;
+    }
     check_layout(s, b, b.nodes, 0);
     // the 8 octant layouts (ptg_render.hip: one per ray-direction octant):
     // octant 0 is the build order; in octant k every inner node whose split
@@ -261,6 +271,18 @@ int main()
                 for (int c = 0; c < 3; ++c)
                     sp.position[c] = 1.0;
             sp.material = i % 3;
+        }
+        check_scene(s);
+        if (fails)
+            return 1;
+    }
+    {  // every sphere huge: the BVH path with an empty tree
+        std::vector<ptg_sphere> s(70);
+        for (int i = 0; i < 70; ++i) {
+            std::memset(&s[i], 0, sizeof(ptg_sphere));
+            s[i].radius = 1000.0 + i;
+            s[i].position[0] = 3000.0 * std::cos(i * 0.09);
+            s[i].position[2] = 3000.0 * std::sin(i * 0.09);
         }
         check_scene(s);
         if (fails)

@@ -21,4 +21,4 @@ def test_bvh_builder_invariants(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = r.stdout.strip().splitlines()
-    assert len(lines) == 5 and all(line.startswith("ok ") for line in lines), r.stdout
+    assert len(lines) == 6 and all(line.startswith("ok ") for line in lines), r.stdout
