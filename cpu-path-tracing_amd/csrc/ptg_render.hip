@@ -470,10 +470,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // plane, so another wall can only win if its plane is nearer than the
         // winner's root (checked with a 2^-12 margin, far above the roots'
         // rounding): those walls are tested only where that check fails
-        // (rare: rays hitting near an edge), and origins outside the room
-        // test every wall.
-        const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
-                             (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
+        // (rare: rays hitting near an edge); a wall the ray moves away from
+        // only from beyond its tangent plane (below).
         // wall table after the sentinel: byte offsets of the records of axis
         // k's + wall (2k) and - wall (2k + 1), -1 where missing
         const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
@@ -515,23 +513,40 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // compiled to three dependent global loads)
             need[k] = (k != kn) & (u[k] < HUGE_VALF) & !(bn * v[k] < u[k] * bqm);
         }
+        // a wall the ray moves away from can be hit only from beyond its
+        // tangent plane (outside the room's bound on that side -- after a
+        // bounce off a curved wall far from its tangent point, frequent in
+        // box_mirror's mirror tube); a missing wall's bound is +-kFarPlane
+        const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
+                             (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             PTG_STAT(3);
-            if (!in_room) {
-                for (; i < A.end_ax[0]; ++i)
-                    test(i, std::integral_constant<int, kAxX>{});
-                for (; i < A.end_ax[1]; ++i)
-                    test(i, std::integral_constant<int, kAxY>{});
-                for (; i < A.end_ax[2]; ++i)
-                    test(i, std::integral_constant<int, kAxZ>{});
-            } else {
-                auto wall = [&](int k) { return rec_at(walls[2 * k + (comp(d, k) >= 0.0f ? 0 : 1)]); };
-                if (need[0])
-                    test_rec(wall(0), std::integral_constant<int, kAxX>{});
-                if (need[1])
-                    test_rec(wall(1), std::integral_constant<int, kAxY>{});
-                if (need[2])
-                    test_rec(wall(2), std::integral_constant<int, kAxZ>{});
+            auto wall = [&](int k, bool toward) {
+                return rec_at(walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)]);
+            };
+            if (need[0])
+                test_rec(wall(0, true), std::integral_constant<int, kAxX>{});
+            if (need[1])
+                test_rec(wall(1, true), std::integral_constant<int, kAxY>{});
+            if (need[2])
+                test_rec(wall(2, true), std::integral_constant<int, kAxZ>{});
+            if (__ballot(!in_room) != 0ull) {
+                bool away[3];
+                for (int k = 0; k < 3; ++k) {
+                    float pp = A.plane_plus[k], pm = A.plane_minus[k], lo = A.pair_lo[k], hi = A.pair_hi[k];
+                    asm volatile("" : "+s"(pp), "+s"(pm), "+s"(lo), "+s"(hi));
+                    const float ok = comp(o, k);
+                    const bool pos = comp(d, k) >= 0.0f;
+                    // (the wall's existence checked by value as well: a NaN
+                    // origin must not select a missing wall's record)
+                    away[k] = pos ? (!(ok >= lo) & (pm > -HUGE_VALF)) : (!(ok <= hi) & (pp < HUGE_VALF));
+                }
+                if (away[0])
+                    test_rec(wall(0, false), std::integral_constant<int, kAxX>{});
+                if (away[1])
+                    test_rec(wall(1, false), std::integral_constant<int, kAxY>{});
+                if (away[2])
+                    test_rec(wall(2, false), std::integral_constant<int, kAxZ>{});
             }
         }
         i = A.end_ax[2];
@@ -737,6 +752,7 @@ __device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
     return r;
 }
 
+#if !PTG_BVH_WIDE
 // Box test of one compact record (culling only): slab entry/exit in grid
 // units, padded.
 __device__ __forceinline__ bool box_hit(const u32x4 q, const SlabRay &r, const float tcap)
@@ -753,6 +769,7 @@ __device__ __forceinline__ bool box_hit(const u32x4 q, const SlabRay &r, const f
                                         __builtin_fminf(__builtin_fmaxf(tz1, tz2), tcap));
     return !(t_in > t_out * 1.0001f + 1e-6f);
 }
+#endif
 
 #if PTG_BVH_WIDE
 // Box test of a wide-layout record: binary16 planes on the wide grid, stored

@@ -1057,14 +1057,21 @@ static int box_walls_B(const sphB *s, int n, f3 o, f3 d, float a, float *bn, flo
     int need[3];
     for (int k = 0; k < 3; ++k) /* a missing wall: u = inf, never needed; guarded as well */
         need[k] = k != kn && ci[k] >= 0 && !(*bn * v[k] < u[k] * bqm);
-    if (!in_room) {
-        for (int j = 0; j < nw; ++j)
-            test_B(&s[s[j].visit], s[j].visit, o, d, a, bn, bq, id);
-    } else {
-        for (int k = 0; k < 3; ++k)
-            if (need[k])
-                test_B(&s[ci[k]], ci[k], o, d, a, bn, bq, id);
+    for (int k = 0; k < 3; ++k)
+        if (need[k])
+            test_B(&s[ci[k]], ci[k], o, d, a, bn, bq, id);
+    /* a wall the ray moves away from can be hit only from beyond its tangent
+     * plane (outside the room's bound on that side: after a bounce off a
+     * curved wall far from its tangent point); those are tested last */
+    for (int k = 0; k < 3; ++k) {
+        const float ok = fcomp(o, k);
+        const int pos = fcomp(d, k) >= 0.0f;
+        const int w = pos ? rec_minus[k] : rec_plus[k];
+        const int beyond = pos ? !(ok >= lo[k]) : !(ok <= hi[k]);
+        if (w >= 0 && beyond)
+            test_B(&s[w], w, o, d, a, bn, bq, id);
     }
+    (void)in_room;
     return nw;
 }
 
