@@ -402,7 +402,10 @@ struct WideGrid {
     {
         const double g = (v - (double)centre[c]) / (double)scale[c];
         uint16_t h = dir < 0 ? half_floor(g) : half_ceil(g);
-        for (int k = 0; k < 4; ++k) {  // one more half step out while the decoded plane is inside
+        // one more half step out while the decoded plane is inside (at most a
+        // step or two: g's own rounding); child boxes lie in the root box, so
+        // |g| stays far from the binary16 range end (65504)
+        for (int k = 0; k < 64; ++k) {
             const double back = (double)centre[c] + half_value(h) * (double)scale[c];
             if (dir < 0 ? back <= v : back >= v)
                 break;
