@@ -100,6 +100,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_CHUNK
 #define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
 #endif
+#ifndef PTG_LEAF_DONE_SEL
+#define PTG_LEAF_DONE_SEL 1  // BVH (wide): leaf completion by selects for the whole wave, not divergent branches
+#endif
 #ifndef PTG_BVH_UNIT_MULT
 #define PTG_BVH_UNIT_MULT 2  // BVH scenes below the split-tail threshold: this many times more work units (8-way C5 shards: 2 beats 1 and 4 by 2-5 %)
 #endif
@@ -847,6 +850,41 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     }
     tr.ni = next;
 }
+
+#if PTG_LEAF_DONE_SEL
+// The render kernel's leaf completion (bvh_leaf_done) and its pop, executed
+// by every lane of the wave: lanes without a tested leaf (act false) keep
+// their state through selects.  As nested divergent branches the update
+// merged the traversal state through exec-masked copies (39 v_mov per leaf
+// phase in the ISA); same values, C5 -0.5 %.
+//
+// Pop where need (else return keep): the stack top, or once it runs dry the
+// resume position and its continuation -- the one load stays behind a branch
+// (rare: the two-entry stack overflowed earlier).
+__device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bool need, const int keep)
+{
+    const int v = tr.s0, r = tr.res;
+    const bool dry = v == -1;
+    int nres = r;
+    if (need & dry & (r != -1))
+        nres = cont[r >> 2];
+    tr.s0 = need ? tr.s1 : v;
+    tr.s1 = need ? -1 : tr.s1;
+    tr.res = nres;
+    return need ? (dry ? r : v) : keep;
+}
+
+// bvh_leaf_done for the lanes whose parked leaf was tested (act)
+__device__ __forceinline__ void bvh_leaf_done_sel(gptr<int> cont, BvhTrav &tr, const bool act)
+{
+    tr.pend = act ? -1 : tr.pend;
+    int next = bvh_pop_sel(cont, tr, act && tr.ni == kPopLater, tr.ni);
+    const bool lf = act && next < kPopLater;  // a leaf word (popped, or waiting in ni)
+    tr.pend = lf ? (next & 0x7FFFFFFF) : tr.pend;
+    next = lf ? kPopLater : next;
+    tr.ni = act ? next : tr.ni;
+}
+#endif
 #else
 // One node step: test node tr.ni's box; hit -> descend (ni + 1; a leaf is
 // parked in tr.pend), miss -> skip the subtree.
@@ -999,11 +1037,17 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
         update_lex(htb, hbest, tb, best);
         update_lex(htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
     }
+#if PTG_BVH_WIDE && PTG_LEAF_DONE_SEL
+    tr.tb = has ? tb : tr.tb;
+    tr.best = has ? best : tr.best;
+    bvh_leaf_done_sel(cont, tr, has);
+#else
     if (has) {
         tr.tb = tb;
         tr.best = best;
         bvh_leaf_done(cont, tr);
     }
+#endif
 }
 
 // Whole scan of one ray (parity probe kernel): walk, testing each parked leaf
@@ -1562,16 +1606,16 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         PTG_PHASE(2);
                     } else {
                         PTG_PHASE(5);
-                        if (trv && tr.pend < 0) {  // node step
 #if PTG_SLAB_PER_STEP
-                            const SlabRay sr = slab_ray(A, o, d);  // recomputed: 6 VGPRs fewer across the walk
+                        const SlabRay sr = slab_ray(A, o, d);  // recomputed: 6 VGPRs fewer across the walk
 #endif
+                        // (the node step as selects for the whole wave, like the leaf
+                        // completion: +2.3 % -- its loads and selects for idle lanes)
+                        if (trv && tr.pend < 0)  // node step
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
-                        }
                         PTG_PHASE(1);
                     }
-                    if (trv && bvh_done(A, tr))
-                        phase = 2;
+                    phase = (trv && bvh_done(A, tr)) ? 2 : phase;
                 }
             }
 #if PTG_WAVE_STATS == 2  // debug: wave-level main-loop iterations / iterations that shade (first active lane)
