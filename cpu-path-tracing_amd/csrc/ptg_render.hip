@@ -966,8 +966,9 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 // the one-lane result bit for bit.  pair: 2 x 64 bytes of LDS (owner lane by
 // owner rank, helper lane by helper rank).
 template <bool kCount>
-__device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f3 o, f3 d, bool has, BvhTrav &tr,
-                                               ScanCount &cnt, uint8_t (*pair)[64])
+__device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f3 o, f3 d, bool has,
+                                               unsigned long long mhas, BvhTrav &tr, ScanCount &cnt,
+                                               uint8_t (*pair)[64])
 {
     const int lane = (int)__lane_id();
     const int nl = has ? (tr.pend >> 24) : 0;
@@ -976,7 +977,8 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
         return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
     };
     const bool longl = nl >= 4;
-    const unsigned long long ml = __ballot(longl), ms = __ballot(own && !longl), mh = __ballot(hlp);
+    // (mhas = ballot(has), the whole wave active: ballots of single compares only)
+    const unsigned long long ml = __ballot(longl), ms = __ballot(own) & ~ml, mh = ~mhas;
     const int nlong = (int)__popcll(ml), nown = nlong + (int)__popcll(ms), nhelp = (int)__popcll(mh);
     const int np1 = min(nown, nhelp);  // owners (by rank) with a first helper
 #if PTG_LEAF_SPLIT >= 2
@@ -1569,16 +1571,22 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
 #if !PTG_SLAB_PER_STEP
                 const SlabRay sr = slab_ray(A, o, d);
 #endif
+                const int na = (int)__popcll(__ballot(item >= 0));
                 for (;;) {
-                    const bool trv = item >= 0 && phase == 1;
+                    // ballots of single compares: a ballot of a combined
+                    // predicate (x && y) was materialised as v_cndmask + v_cmp,
+                    // 2 VALU each, 3 per walk iteration.  phase 1 implies
+                    // item >= 0 (an item ends only in shading, from phase 2),
+                    // and na does not change inside the walk.
+                    const bool trv = phase == 1;
                     const unsigned long long mt = __ballot(trv);
                     if (mt == 0ull)
                         break;
                     const int nt = (int)__popcll(mt);
-                    const int na = (int)__popcll(__ballot(item >= 0));
                     if (8 * (na - nt) >= PTG_READY_FRAC * na)
                         break;
-                    const int nh = (int)__popcll(__ballot(trv && tr.pend >= 0));
+                    const unsigned long long mhas = __ballot(tr.pend >= 0) & mt;  // walking lanes holding a leaf
+                    const int nh = (int)__popcll(mhas);
 #if PTG_WAVE_STATS == 1  // debug: wave-level node steps / leaf sphere iterations (first active lane only)
                     if constexpr (kCount) {
                         const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
@@ -1597,8 +1605,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         // with ds_bpermute + LDS atomicMin measured 1.7 % slower; pairing
                         // idle lanes with the long leaves, below, 1.2-1.5 % faster)
 #if PTG_LEAF_SPLIT
-                        bvh_leaf_split<kCount && !PTG_WAVE_STATS>(A, cont, o, d, trv && tr.pend >= 0, tr, scnt,
-                                                                   lds_pair[wv]);
+                        bvh_leaf_split<kCount && !PTG_WAVE_STATS>(A, cont, o, d, trv && tr.pend >= 0, mhas, tr,
+                                                                   scnt, lds_pair[wv]);
 #else
                         if (trv && tr.pend >= 0)
                             bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
