@@ -94,9 +94,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_SPLIT
 #define PTG_LEAF_SPLIT 2  // BVH leaf phase: lanes without a leaf test part of another lane's leaf (1: one helper per leaf, 2: up to two)
 #endif
-#ifndef PTG_SLAB_PER_STEP
-#define PTG_SLAB_PER_STEP 0  // BVH: the ray's slab constants recomputed per node step instead of held across the walk
-#endif
 #ifndef PTG_LEAF_CHUNK
 #define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
 #endif
@@ -1568,61 +1565,57 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             }
             PTG_PHASE(0);
             {
-#if !PTG_SLAB_PER_STEP
                 const SlabRay sr = slab_ray(A, o, d);
-#endif
                 const int na = (int)__popcll(__ballot(item >= 0));
+                // Node steps in an inner loop, the leaf phase in the outer one:
+                // with both in one loop body, the merge of the two branches'
+                // traversal states cost 14+ v_mov per node step (the compiler
+                // copied the 7 state registers out and back in; C5 -1.5 %).
                 for (;;) {
-                    // ballots of single compares: a ballot of a combined
-                    // predicate (x && y) was materialised as v_cndmask + v_cmp,
-                    // 2 VALU each, 3 per walk iteration.  phase 1 implies
-                    // item >= 0 (an item ends only in shading, from phase 2),
-                    // and na does not change inside the walk.
-                    const bool trv = phase == 1;
-                    const unsigned long long mt = __ballot(trv);
-                    if (mt == 0ull)
-                        break;
-                    const int nt = (int)__popcll(mt);
-                    if (8 * (na - nt) >= PTG_READY_FRAC * na)
-                        break;
-                    const unsigned long long mhas = __ballot(tr.pend >= 0) & mt;  // walking lanes holding a leaf
-                    const int nh = (int)__popcll(mhas);
-#if PTG_WAVE_STATS == 1  // debug: wave-level node steps / leaf sphere iterations (first active lane only)
-                    if constexpr (kCount) {
-                        const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
-                        if (8 * nh >= PTG_LEAF_FRAC * nt) {
-                            int mx = trv && tr.pend >= 0 && !PTG_LEAF_SPLIT ? (tr.pend >> 24) : 0;  // split: counted there
-                            for (int off = 32; off > 0; off >>= 1)
-                                mx = max(mx, __shfl_xor(mx, off, 64));
-                            scnt.spheres += first_lane ? mx : 0;
-                        } else {
-                            scnt.boxes += first_lane ? 1 : 0;
+                    unsigned long long mhas = 0ull;
+                    bool walk_done = false;
+                    for (;;) {
+                        // ballots of single compares: a ballot of a combined
+                        // predicate (x && y) is materialised as v_cndmask + v_cmp,
+                        // 2 VALU each.  phase 1 implies item >= 0 (an item ends
+                        // only in shading, from phase 2), and na does not change
+                        // inside the walk.
+                        const bool trv = phase == 1;
+                        const unsigned long long mt = __ballot(trv);
+                        const int nt = (int)__popcll(mt);
+                        if (mt == 0ull || 8 * (na - nt) >= PTG_READY_FRAC * na) {
+                            walk_done = true;
+                            break;
                         }
-                    }
+                        mhas = __ballot(tr.pend >= 0) & mt;  // walking lanes holding a leaf
+                        if (8 * (int)__popcll(mhas) >= PTG_LEAF_FRAC * nt)
+                            break;  // leaf phase
+#if PTG_WAVE_STATS == 1  // debug: wave-level node steps (first active lane only)
+                        if constexpr (kCount)
+                            scnt.boxes += __lane_id() == __ffsll((long long)__ballot(1)) - 1 ? 1 : 0;
 #endif
-                    if (8 * nh >= PTG_LEAF_FRAC * nt) {  // leaf phase
-                        // (round 1: spreading the parked leaves' spheres over the whole wave
-                        // with ds_bpermute + LDS atomicMin measured 1.7 % slower; pairing
-                        // idle lanes with the long leaves, below, 1.2-1.5 % faster)
-#if PTG_LEAF_SPLIT
-                        bvh_leaf_split<kCount && !PTG_WAVE_STATS>(A, cont, o, d, trv && tr.pend >= 0, mhas, tr,
-                                                                   scnt, lds_pair[wv]);
-#else
-                        if (trv && tr.pend >= 0)
-                            bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
-#endif
-                        PTG_PHASE(2);
-                    } else {
                         PTG_PHASE(5);
-#if PTG_SLAB_PER_STEP
-                        const SlabRay sr = slab_ray(A, o, d);  // recomputed: 6 VGPRs fewer across the walk
-#endif
-                        // (the node step as selects for the whole wave, like the leaf
-                        // completion: +2.3 % -- its loads and selects for idle lanes)
-                        if (trv && tr.pend < 0)  // node step
+                        // (the node step as selects for the whole wave, like the
+                        // leaf completion: +2.3 % -- its loads and selects for idle lanes)
+                        if (trv && tr.pend < 0)
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
                         PTG_PHASE(1);
+                        phase = (trv && bvh_done(A, tr)) ? 2 : phase;
                     }
+                    if (walk_done)
+                        break;
+                    // leaf phase (round 1: spreading the parked leaves' spheres over
+                    // the whole wave with ds_bpermute + LDS atomicMin measured 1.7 %
+                    // slower; pairing idle lanes with the long leaves 1.2-1.5 % faster)
+                    const bool trv = phase == 1;
+#if PTG_LEAF_SPLIT
+                    bvh_leaf_split<kCount && !PTG_WAVE_STATS>(A, cont, o, d, trv && tr.pend >= 0, mhas, tr, scnt,
+                                                               lds_pair[wv]);
+#else
+                    if (trv && tr.pend >= 0)
+                        bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
+#endif
+                    PTG_PHASE(2);
                     phase = (trv && bvh_done(A, tr)) ? 2 : phase;
                 }
             }
