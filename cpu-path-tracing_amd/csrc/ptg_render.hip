@@ -612,25 +612,19 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
     }
     if (disc < 0.0f)
         return kReject;
-    float sq = sqrt_scan(disc);  // disc >= 0 here
-    float num, den;
-    if (hb < 0.0f) {
-        float q = sq - hb;
-        num = c;
-        den = q;
-        if (c < kEps * q) {
-            num = q;
-            den = a;
-            if (q < kEps * a)
-                return kReject;
-        }
-    } else {
-        float qn = hb + sq;
-        num = -c;
-        den = qn;
-        if (num < kEps * den)
-            return kReject;
-    }
+    const float sq = sqrt_scan(disc);  // disc >= 0 here
+    // the near root c/q (hb < 0, q = sq - hb), else the far root q/a, or -c/qn
+    // (hb >= 0, qn = hb + sq) -- as selects (scene_scan's form: sq - hb and
+    // hb + sq are the IEEE add sq + |hb|; one eps test covers the three cases),
+    // not two divergent branches that a wave with both signs ran one after
+    // the other
+    const bool neg = hb < 0.0f;
+    const float qq = sq + __builtin_fabsf(hb);
+    const bool near_lt = c < kEps * qq;
+    const float num = neg ? (near_lt ? qq : c) : -c;
+    const float den = (neg & near_lt) ? a : qq;
+    if (num < kEps * den)
+        return kReject;
     return num / den;
 }
 
