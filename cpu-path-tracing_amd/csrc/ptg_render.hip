@@ -1324,6 +1324,21 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     // the camera code runs only in refills of >= PTG_REFILL_BATCH lanes (or
     // when a lane would otherwise idle).
     __shared__ float4 lds_pre[kWaves][64][2];
+    // the lane's own record.  BVH kernel: its address formed at each use
+    // (v_mbcnt of an opaque all-ones mask: not hoisted), not held in a VGPR
+    // for the unit -- at 64 VGPRs it had been spilled and reloaded in the main
+    // loop (C5 -0.3 %; the linear kernel, with VGPRs to spare, is 1.4 % slower
+    // that way)
+    auto pre_rec = [&]() -> float4 * {
+        if constexpr (kBvh) {
+            unsigned ones = ~0u;
+            asm volatile("" : "+s"(ones));
+            const unsigned ln = __builtin_amdgcn_mbcnt_hi(ones, __builtin_amdgcn_mbcnt_lo(ones, 0u));
+            return lds_pre[wv][ln];
+        } else {
+            return lds_pre[wv][lane];
+        }
+    };
     // it / nv and it % nv (it < 2^24, only for a unit of fewer than 64
     // slots) through a float reciprocal formed at each use: the compiler's
     // integer division by the unit's nv kept its constants in VGPRs for the
@@ -1380,11 +1395,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         depth = 0;
     };
     auto store_pre = [&](int it, f3 ro, f3 rd, uint32_t rs) {
-        lds_pre[wv][lane][0] = make_float4(ro.x, ro.y, rd.x, rd.y);
+        float4 *rec = pre_rec();
+        rec[0] = make_float4(ro.x, ro.y, rd.x, rd.y);
         // ro.z (= the camera's z, the lens offset has no z) rides in the
         // record's last word: read back with the ray, not as a kernel
         // argument (a scalar load + wait in the path-start block)
-        lds_pre[wv][lane][1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), ro.z);
+        rec[1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), ro.z);
     };
     if (item >= 0) {
         f3 ro, rd;
@@ -1418,11 +1434,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     // which forces a batch; there its E is parked, and it starts a new ray.
     bool parked = false;
     auto park = [&]() {
-        lds_pre[wv][lane][0] = make_float4(E.x, E.y, E.z, __int_as_float(slot));
+        pre_rec()[0] = make_float4(E.x, E.y, E.z, __int_as_float(slot));
         parked = true;
     };
     auto flush_parked = [&]() {
-        const float4 pk = lds_pre[wv][lane][0];
+        const float4 pk = pre_rec()[0];
         flush(pk.x, pk.y, pk.z, __float_as_int(pk.w));
         parked = false;
     };
@@ -1430,7 +1446,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     auto path_done = [&]() {
         item = -1;
         if (has_pre) {
-            const float4 p0 = lds_pre[wv][lane][0], p1 = lds_pre[wv][lane][1];
+            const float4 *rec = pre_rec();
+            const float4 p0 = rec[0], p1 = rec[1];
             park();
             begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
             has_pre = false;
