@@ -673,7 +673,7 @@ struct BvhTrav {
 };
 
 #if PTG_BVH_WIDE
-__device__ __forceinline__ bool bvh_done(const KArgs &, const BvhTrav &tr) { return tr.ni == -1 && tr.pend < 0; }
+__device__ __forceinline__ bool bvh_done(const KArgs &, const BvhTrav &tr) { return (tr.ni == -1) & (tr.pend < 0); }
 __device__ __forceinline__ int bvh_pop(gptr<int> cont, BvhTrav &tr)
 {
     const int v = tr.s0;
@@ -1611,7 +1611,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         if (trv && tr.pend < 0)
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
                         PTG_PHASE(1);
-                        phase = (trv && bvh_done(A, tr)) ? 2 : phase;
+                        phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
                     }
                     if (walk_done)
                         break;
@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
 #endif
                     PTG_PHASE(2);
-                    phase = (trv && bvh_done(A, tr)) ? 2 : phase;
+                    phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
                 }
             }
 #if PTG_WAVE_STATS == 2  // debug: wave-level main-loop iterations / iterations that shade (first active lane)
