@@ -634,11 +634,11 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
 // (intersect_B_lex) gives the same bits.
 __device__ __forceinline__ void update_lex(const float t, const int sid, float &tb, int &best)
 {
-    // t <= tb: NaN (rejected) fails; (unsigned) -1 orders after every index
-    if (t <= tb && (t < tb || (unsigned)sid < (unsigned)best)) {
-        tb = t;
-        best = sid;
-    }
+    // a NaN t (rejected) fails both compares; (unsigned) -1 orders after every
+    // index.  Selects, not a short-circuit && / || (exec-masked blocks)
+    const bool win = (t < tb) | ((t == tb) & ((unsigned)sid < (unsigned)best));
+    tb = win ? t : tb;
+    best = win ? sid : best;
 }
 
 // Per-lane BVH scan state.  The render kernel keeps it across iterations of
@@ -821,14 +821,14 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     };
     const unsigned r1 = m & (m - 1u);  // hits after the first
     const int wf = lowest(m), ws = lowest(r1);
-    const bool leaf = m != 0u && wf < kPopLater;  // the first hit is a leaf: parked
+    const bool leaf = (m != 0u) & (wf < kPopLater);  // the first hit is a leaf: parked
     const unsigned rest = leaf ? r1 & (r1 - 1u) : r1;
     int next = m == 0u ? -1 : leaf ? (r1 != 0u ? ws : kPopLater) : wf;
     tr.pend = leaf ? (wf & 0x7FFFFFFF) : tr.pend;
     const int pos = base + (int)__builtin_ctz(rest | 16u);
     const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
     const bool push = rest != 0u, full = tr.s1 != -1;
-    tr.res = (push && full) ? pos : tr.res;
+    tr.res = (push & full) ? pos : tr.res;
     const int s0 = tr.s0;
     tr.s0 = push ? (full ? -1 : e) : s0;
     tr.s1 = push ? (full ? -1 : s0) : tr.s1;
@@ -869,8 +869,8 @@ __device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bo
 __device__ __forceinline__ void bvh_leaf_done_sel(gptr<int> cont, BvhTrav &tr, const bool act)
 {
     tr.pend = act ? -1 : tr.pend;
-    int next = bvh_pop_sel(cont, tr, act && tr.ni == kPopLater, tr.ni);
-    const bool lf = act && next < kPopLater;  // a leaf word (popped, or waiting in ni)
+    int next = bvh_pop_sel(cont, tr, act & (tr.ni == kPopLater), tr.ni);
+    const bool lf = act & (next < kPopLater);  // a leaf word (popped, or waiting in ni)
     tr.pend = lf ? (next & 0x7FFFFFFF) : tr.pend;
     next = lf ? kPopLater : next;
     tr.ni = act ? next : tr.ni;
@@ -979,7 +979,7 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
 #endif
     const int ro = longl ? rank(ml) : nlong + rank(ms);
     const int rh = rank(mh);
-    const bool po = own && ro < np1, ph = hlp && rh < np1 + np2;
+    const bool po = own & (ro < np1), ph = hlp & (rh < np1 + np2);
     if (po)
         pair[0][ro] = (uint8_t)lane;
     if (ph)
@@ -990,7 +990,7 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     const int orank = rh < np1 ? rh : rh - np1;  // a helper's owner, and which helper it is
     const int part = rh < np1 ? 1 : 2;
     const int partner = po ? (int)pair[1][ro] : ph ? (int)pair[0][orank] : lane;
-    const int partner2 = (po && ro < np2) ? (int)pair[1][np1 + ro] : lane;
+    const int partner2 = (po & (ro < np2)) ? (int)pair[1][np1 + ro] : lane;
     auto bpf = [](int who, float v) {
         return __int_as_float(__builtin_amdgcn_ds_bpermute(who << 2, __float_as_int(v)));
     };
