@@ -1112,17 +1112,23 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // are loaded and selected (3 selects instead of address arithmetic)
     const float4 c2 = S.s2, c3 = S.s3;
     const bool rr = depth > kRRThreshold;
-    if (rr && !(draw(st) < s0.w))
-        return true;
+    // Russian roulette without an early return: the roulette's draw advances the state of the
+    // rr lanes only (a select), and a killed lane runs on with its materials
+    // masked -- its next ray and state are discarded (the early return's
+    // merge had cost state copies and exec-mask blocks)
+    uint32_t st_rr = st;
+    const float u_rr = draw(st_rr);
+    st = rr ? st_rr : st;
+    const bool killed = rr & !(u_rr < s0.w);  // (box -0.6 %, box_mirror -1.0 %)
     T = mk3(T.x * (rr ? c3.x : c2.x), T.y * (rr ? c3.y : c2.y), T.z * (rr ? c3.z : c2.z));
     // BRDF samplers (main.cpp:44-97).  Diffuse and dielectric lanes share the
     // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
     // holding both materials issues them once; every lane's arithmetic is the
     // same as the per-material code (oracle sample_B).
     const int mat = __float_as_int(s1.w);
-    const bool isD = mat == PTG_DIFFUSE;
-    const bool isG = mat == PTG_DIELECTRIC;
-    bool spec = mat == PTG_SPECULAR;
+    const bool isD = !killed & (mat == PTG_DIFFUSE);
+    const bool isG = !killed & (mat == PTG_DIELECTRIC);
+    bool spec = !killed & (mat == PTG_SPECULAR);
     f3 nd = d;  // every lane sets it below (mirror lanes in the spec block)
     // a wave with only mirror lanes skips the diffuse/dielectric work
     // (wave-uniform, exact: those lanes' values are all overwritten)
@@ -1184,7 +1190,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     o = p;
     d = nd;
     depth += 1;
-    return depth >= kDepthLimit;
+    return killed | (depth >= kDepthLimit);
 }
 
 // Slab row -> image (output) row for the band shard.
