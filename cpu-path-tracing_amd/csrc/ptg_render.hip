@@ -2620,8 +2620,11 @@ int ptg_context_destroy(ptg_context *ctx)
 namespace {
 
 // exact accumulator: allocated (zeroed) on first use at a size; resolve_kernel
-// keeps it zero between one-shot frames
-int ensure_acc(ptg_context *ctx, size_t need)
+// keeps it zero between one-shot frames.  The zeroing is queued on the launch
+// stream: a hipMemset on the null stream is not ordered before kernels on a
+// non-blocking stream (ptg_render_multi's), whose first frame could then add
+// into a buffer being cleared (seen once as a differing box_mirror frame)
+int ensure_acc(ptg_context *ctx, size_t need, hipStream_t stream)
 {
     if (need <= ctx->acc_elems)
         return PTG_OK;
@@ -2631,7 +2634,7 @@ int ensure_acc(ptg_context *ctx, size_t need)
     ctx->acc_elems = 0;
     if (hipMalloc(&ctx->d_acc, need * sizeof(unsigned long long)) != hipSuccess)
         return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the accumulator failed");
-    PTG_HIP(hipMemset(ctx->d_acc, 0, need * sizeof(unsigned long long)));
+    PTG_HIP(hipMemsetAsync(ctx->d_acc, 0, need * sizeof(unsigned long long), stream));
     ctx->acc_elems = need;
     ctx->acc_dirty = false;  // (a progressive frame in the old buffer is lost: reset before reuse)
     return PTG_OK;
@@ -2720,12 +2723,12 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
         return launch_ref64(ctx, A, nullptr, d_slab, d_segments, reinterpret_cast<hipStream_t>(stream));
     // several units per pixel, a split tail accumulated in HBM, or no samples at all
     const bool resolve = A.needs_resolve || grid == 0;
-    if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0)))
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if ((rc = ensure_acc(ctx, resolve ? acc_elems_for(A) : 0, s)))
         return rc;
     A.out = d_slab;
     A.acc = ctx->d_acc;
     A.segments = d_segments;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (resolve && ctx->acc_dirty) {
         // progressive sums left by accumulate / keep_acc resolve: a one-shot
         // frame starts from zero (its resolve leaves the buffer zero again)
@@ -2755,7 +2758,7 @@ int ptg_accumulate_device(ptg_context *ctx, const ptg_params *params, int32_t sa
     int grid = 0;
     if ((rc = fill_launch(ctx, params, A, grid, sample_begin, sample_end, /*accumulate_only=*/true)))
         return rc;
-    if ((rc = ensure_acc(ctx, acc_elems_for(A))))
+    if ((rc = ensure_acc(ctx, acc_elems_for(A), reinterpret_cast<hipStream_t>(stream))))
         return rc;
     A.acc = ctx->d_acc;
     A.segments = d_segments;
@@ -2777,7 +2780,7 @@ int ptg_resolve_device(ptg_context *ctx, const ptg_params *params, int32_t sampl
     int grid = 0;
     if ((rc = fill_launch(ctx, params, A, grid)))
         return rc;
-    if ((rc = ensure_acc(ctx, acc_elems_for(A))))
+    if ((rc = ensure_acc(ctx, acc_elems_for(A), reinterpret_cast<hipStream_t>(stream))))
         return rc;
     A.samps = samples_done;  // mean over the samples accumulated so far
     A.keep_acc = 1;
@@ -2799,7 +2802,7 @@ int ptg_reset_accumulation_device(ptg_context *ctx, const ptg_params *params, vo
     int grid = 0;
     if ((rc = fill_launch(ctx, params, A, grid)))
         return rc;
-    if ((rc = ensure_acc(ctx, acc_elems_for(A))))
+    if ((rc = ensure_acc(ctx, acc_elems_for(A), reinterpret_cast<hipStream_t>(stream))))
         return rc;
     PTG_HIP(hipMemsetAsync(ctx->d_acc, 0, ctx->acc_elems * sizeof(unsigned long long),
                            reinterpret_cast<hipStream_t>(stream)));
