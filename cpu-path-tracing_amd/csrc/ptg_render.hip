@@ -89,7 +89,7 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #define PTG_REFILL_BATCH 40  // measured: 40 beats 32 by 0.35 % (box) / 0.6 % (box_mirror), ties 48-56; 24 is 1.2 % slower
 #endif
 #ifndef PTG_LEAF_FRAC
-#define PTG_LEAF_FRAC 5  // BVH: leaf phase once 5/8 of the walking lanes hold a leaf (wide walk + leaf pairing: 5 beats 6 by 0.9 %, 7 by 3 %)
+#define PTG_LEAF_FRAC 4  // BVH: leaf phase once 4/8 of the walking lanes hold a leaf (re-swept after the walk clean-up: 4 and 3 beat 5 by 0.6 %, 6 +1.5 %)
 #endif
 #ifndef PTG_LEAF_SPLIT
 #define PTG_LEAF_SPLIT 2  // BVH leaf phase: lanes without a leaf test part of another lane's leaf (1: one helper per leaf, 2: up to two)
