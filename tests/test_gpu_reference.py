@@ -235,3 +235,27 @@ def test_sunk_spheres_image_bitexact():
     gpu = _render(scn, cam, W, H, samps)
     ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, nthreads=NT)
     assert np.array_equal(gpu, ref)
+
+
+@pytest.mark.gpu
+def test_fresh_contexts_on_side_streams():
+    """A fresh context's first frame on a non-blocking stream (torch side
+    streams are created non-blocking): the accumulator's first zeroing is
+    queued on that stream (ensure_acc), not on the null stream, which such a
+    stream does not wait for.  Frames with an HBM-accumulated split tail and
+    with sample chunks, several fresh contexts each, equal the frame rendered
+    on the current stream bit for bit."""
+    _require_gpu()
+    for W, H, samps, chunk in ((1920, 1080, 4, 0), (48, 30, 16, 3)):
+        scn = ptgpu.box_mirror_scene(W, H)
+        cam = ptgpu.camera.with_config(scn.camera_parameters)
+        p = ptgpu.make_params(W, H, samps, 2, SEED, chunk_samples=chunk)
+        ref = _render_chunked(scn, cam, W, H, samps, chunk)
+        for _ in range(4):
+            side = torch.cuda.Stream()
+            out = torch.full((H * W * 3,), -7.0, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            with ptgpu.Context(scn, cam) as ctx:
+                ctx.render_device(out, p, stream=side)
+                side.synchronize()
+            assert np.array_equal(out.cpu().numpy().reshape(H, W, 3), ref)
