@@ -97,6 +97,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_CHUNK
 #define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
 #endif
+#ifndef PTG_LONG_LEAF
+#define PTG_LONG_LEAF 5  // BVH leaf phase: leaves of at least this many spheres get helpers first (and a second one; 5 beats 4 by 0.9 %, 3 and 6 worse)
+#endif
 #ifndef PTG_LEAF_DONE_SEL
 #define PTG_LEAF_DONE_SEL 1  // BVH (wide): leaf completion by selects for the whole wave, not divergent branches
 #endif
@@ -949,7 +952,7 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 
 // Leaf phase with helpers (PTG_LEAF_SPLIT; called by the whole wave): lanes
 // with no leaf to test are assigned, by rank, to lanes holding a leaf of >= 2
-// spheres -- one helper per such leaf, longest leaves (>= 4 spheres: they set
+// spheres -- one helper per such leaf, longest leaves (>= PTG_LONG_LEAF spheres: they set
 // the wave's loop length) first, then a second helper per long leaf while
 // idle lanes remain.  A helper tests its part of the leaf with the owner's
 // ray and culling distance (ds_bpermute) and the owner merges the helpers'
@@ -967,7 +970,7 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     auto rank = [](unsigned long long m) {
         return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
     };
-    const bool longl = nl >= 4;
+    const bool longl = nl >= PTG_LONG_LEAF;
     // (mhas = ballot(has), the whole wave active: ballots of single compares only)
     const unsigned long long ml = __ballot(longl), ms = __ballot(own) & ~ml, mh = ~mhas;
     const int nlong = (int)__popcll(ml), nown = nlong + (int)__popcll(ms), nhelp = (int)__popcll(mh);
