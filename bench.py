@@ -8,10 +8,11 @@ sub-pixel); with N > 1 ranks (torchrun, one process per GPU) BASELINE.json
 configs[3] = C4, box_scene at 3840x2160, 4096 spp, tile-sharded by
 interleaved row bands, the step including the single gather (RCCL over xGMI)
 to rank 0 and the un-shard.  value = whole-frame samples / max-over-ranks time
-(strong scaling: the frame is fixed for a given N; C4 on one GPU runs at the
-same per-sample rate as the 1080p frame, 12.35 vs 12.4 G samples/s in round 1,
-so the per-N values compare).  --workload c1..c5 / bench pick one config for
-every N.
+(strong scaling: the frame is fixed for a given N).  At N > 1 rank 0 first
+renders the same frame alone (untimed for `value`) and the line carries
+t1_ms and efficiency = T1 / (N * T_N) of this run, so the scaling line is
+self-contained (the N = 1 default line is the metric's 1080p frame).
+--workload c1..c5 / bench pick one config for every N.
 
 Also reported:
   roofline     -- VALU fp32 roofline of the render kernel: algorithmic FLOP
@@ -194,6 +195,8 @@ def main():
                     help="CPU baseline: time every k-th row of the frame (8 = one eighth)")
     ap.add_argument("--reference-f64", action="store_true",
                     help="PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode, not the metric)")
+    ap.add_argument("--t1", choices=["auto", "off"], default="auto",
+                    help="N > 1: time the same frame on rank 0's GPU alone first (t1_ms, efficiency)")
     ap.add_argument("--quality-rows", type=int, default=4,
                     help="rows checked against the CPU oracle in the cpu_baseline leg (0 = none)")
     args = ap.parse_args()
@@ -259,6 +262,26 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
+
+    # N > 1: the same frame rendered by rank 0 alone (shard_count 1), untimed
+    # with respect to `value` -- the driver's 1-GPU BENCH line is the 1080p
+    # frame, so the N-GPU line carries its own same-frame T1 and efficiency
+    t1 = None
+    if world > 1 and args.t1 == "auto":
+        if rank == 0:
+            p1 = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, 0, 1, args.chunk, flags=f64)
+            full = torch.empty(ptgpu.shard_rows(H, args.band_rows, 1) * W * 3, dtype=torch.float32, device=dev)
+            ctx.render_device(full, p1, None, stream)  # warm-up (allocates the accumulator)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            w0 = time.perf_counter()
+            e0.record(stream)
+            ctx.render_device(full, p1, None, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            t1 = {"ms": round(e0.elapsed_time(e1), 3), "wall_ms": round((time.perf_counter() - w0) * 1e3, 3)}
+            del full
+        dist.barrier()
 
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     if world > 1:
@@ -359,6 +382,11 @@ def main():
         }
         if per_rank is not None:
             out["per_rank"] = per_rank
+        if t1 is not None:
+            # efficiency of this run = T1 / (N * T_N), both on this node in this run
+            out["t1_ms"] = t1["ms"]
+            out["t1"] = dict(t1, note="the same frame on rank 0's GPU alone (HIP events; no gather), untimed for value")
+            out["efficiency"] = round(t1["ms"] / (world * elapsed / args.steps * 1e3), 4)
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)

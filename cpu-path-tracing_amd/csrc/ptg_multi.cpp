@@ -1,162 +1,432 @@
-// ptg_multi.cpp -- single-process multi-GPU frame: the
+// ptg_multi.cpp -- single-process multi-GPU frames: the
 // drop-in ptg_render over several devices of one node, one RCCL gather.
 //
 // Replaces the taskflow row loop (src/main.cpp:214-236) for a C++ caller that
 // owns several GPUs in one process (host/main.cpp --devices): device k renders
 // the interleaved row bands b with b % n == k into a contiguous slab
-// (ptg_render_device, shard_rank = k), ONE ncclGather (rccl.h:745, over xGMI
-// between MI355X devices) collects the slabs on the first device, and
-// ptg_unshard_device restores the row order there.  The RNG is keyed by the
-// global pixel, so the image equals the one-device frame bit for bit.  The
-// multi-process path (one rank per GPU, torch.distributed on RCCL) is
-// ptgpu.render_sharded; both use the same slab layout and un-shard kernel.
+// (ptg_render_device / ptg_resolve_device, shard_rank = k), ONE ncclGather
+// (rccl.h:745, over xGMI between MI355X devices) collects the slabs on the
+// first device, and ptg_unshard_device restores the row order there.  The RNG
+// is keyed by the global pixel, so the image equals the one-device frame bit
+// for bit.
+//
+// A ptg_multi holds, per device, the scene in HBM (a ptg_context), a
+// non-blocking stream and the slab, the RCCL communicator of the device set
+// (ncclCommInitAll once), and on the root the gathered slabs and the image:
+// repeated frames and progressive passes reuse all of it.  ptg_render_multi is
+// create + render + destroy.  The multi-process path (one rank per GPU,
+// torch.distributed on RCCL) is ptgpu.render_sharded; all three use the same
+// slab layout and un-shard kernel.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "../../include/ptgpu.h"
 
-namespace {
-
 // ptg_last_error is thread-local in ptg_render.hip; errors raised here go
 // through the same channel
 extern "C" int ptg_set_error_(int code, const char *msg);
 
+namespace {
+
 int fail(int code, const std::string &msg) { return ptg_set_error_(code, msg.c_str()); }
 
-struct Device {
-    int id = -1;
+struct Shard {
+    int id = -1;  // HIP device
     ptg_context *ctx = nullptr;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // local transport: the slab is complete
     float *slab = nullptr;
+    size_t slab_cap = 0;  // floats
     ncclComm_t comm = nullptr;
 };
 
+// Restores the calling thread's current HIP device on every return path.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&dev) != hipSuccess)
+            dev = -1;
+    }
+    ~DeviceGuard()
+    {
+        if (dev >= 0)
+            (void)hipSetDevice(dev);
+    }
+};
+
+int hip_fail(const char *what, hipError_t e) { return fail(PTG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)); }
+int nccl_fail(const char *what, ncclResult_t r)
+{
+    return fail(PTG_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+#define MULTI_HIP(call)                                                                                 \
+    do {                                                                                                \
+        hipError_t e_ = (call);                                                                         \
+        if (e_ != hipSuccess)                                                                           \
+            return hip_fail(#call, e_);                                                                 \
+    } while (0)
+
 }  // namespace
 
-extern "C" int ptg_render_multi(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam,
-                                const ptg_params *params, const int *devices, int n_devices, double *image_rgb)
+struct ptg_multi {
+    std::vector<Shard> shards;
+    bool rccl = false;  // false: n shards on one device, gathered by device copies (tests)
+    float *gathered = nullptr;  // root: n slabs, rank-major
+    size_t gathered_cap = 0;
+    float *image = nullptr;  // root: the un-sharded frame
+    size_t image_cap = 0;
+    std::vector<float> host;
+};
+
+namespace {
+
+int destroy(ptg_multi *m)
 {
-    if (!params || !image_rgb || !devices || n_devices < 1)
-        return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi: NULL argument or no device");
-    if (params->shard_count != 1 || params->shard_rank != 0)
-        return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi shards the whole frame itself: shard_count must be 1");
+    if (!m)
+        return PTG_OK;
+    DeviceGuard g;
+    for (Shard &s : m->shards) {
+        if (s.id < 0)
+            continue;
+        (void)hipSetDevice(s.id);
+        if (s.stream)
+            (void)hipStreamSynchronize(s.stream);
+    }
+    for (Shard &s : m->shards) {
+        if (s.id < 0)
+            continue;
+        (void)hipSetDevice(s.id);
+        if (s.comm)
+            (void)ncclCommDestroy(s.comm);
+        if (s.slab)
+            (void)hipFree(s.slab);
+        if (s.done)
+            (void)hipEventDestroy(s.done);
+        if (s.stream)
+            (void)hipStreamDestroy(s.stream);
+        if (s.ctx)
+            (void)ptg_context_destroy(s.ctx);
+    }
+    if (!m->shards.empty() && m->shards[0].id >= 0) {
+        (void)hipSetDevice(m->shards[0].id);
+        if (m->gathered)
+            (void)hipFree(m->gathered);
+        if (m->image)
+            (void)hipFree(m->image);
+    }
+    delete m;
+    return PTG_OK;
+}
+
+int create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, const int *devices, int n, bool rccl,
+           ptg_multi **out)
+{
+    if (!out)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi: out is NULL");
+    *out = nullptr;
+    if (!devices || n < 1)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi: no device");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
         return fail(PTG_ERR_NO_DEVICE, "no HIP device visible");
-    for (int k = 0; k < n_devices; ++k) {
+    for (int k = 0; k < n; ++k) {
         if (devices[k] < 0 || devices[k] >= count)
-            return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi: device ordinal out of range");
-        for (int j = 0; j < k; ++j)
+            return fail(PTG_ERR_INVALID_ARGUMENT, "multi: device ordinal out of range");
+        for (int j = 0; j < k && rccl; ++j)
             if (devices[j] == devices[k])
                 return fail(PTG_ERR_UNSUPPORTED, "render_multi: RCCL needs distinct devices (one rank per GPU)");
     }
-    const int W = params->width, H = params->height, BR = params->band_rows, n = n_devices;
+    DeviceGuard g;
+    ptg_multi *m = new ptg_multi();
+    m->rccl = rccl;
+    m->shards.resize(n);
+    int rc = PTG_OK;
+    for (int k = 0; k < n && rc == PTG_OK; ++k) {
+        Shard &s = m->shards[k];
+        s.id = devices[k];
+        if ((rc = ptg_context_create(spheres, n_spheres, cam, s.id, &s.ctx)))
+            break;
+        hipError_t e = hipSetDevice(s.id);
+        if (e == hipSuccess)
+            e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        if (e != hipSuccess)
+            rc = hip_fail("multi: stream/event", e);
+    }
+    if (rc == PTG_OK && rccl) {
+        std::vector<ncclComm_t> cm(n);
+        const ncclResult_t r = ncclCommInitAll(cm.data(), n, devices);
+        if (r != ncclSuccess)
+            rc = nccl_fail("ncclCommInitAll", r);
+        else
+            for (int k = 0; k < n; ++k)
+                m->shards[k].comm = cm[k];
+    }
+    if (rc != PTG_OK) {
+        destroy(m);
+        return rc;
+    }
+    *out = m;
+    return PTG_OK;
+}
+
+int check_frame(const ptg_multi *m, const ptg_params *p)
+{
+    if (!m || !p)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi: NULL context or params");
+    if (p->width <= 0 || p->height <= 0 || p->band_rows < 1)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi: width, height and band_rows must be positive");
+    if (p->shard_count != 1 || p->shard_rank != 0)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi shards the whole frame itself: shard_count must be 1");
+    if (p->flags & PTG_FLAG_REFERENCE_F64)
+        return fail(PTG_ERR_UNSUPPORTED, "render_multi renders the fp32 kernel only (the reference-arithmetic "
+                                         "mode keeps doubles: use ptg_render)");
+    return PTG_OK;
+}
+
+// params of shard k
+ptg_params shard_params(const ptg_params *p, int k, int n)
+{
+    ptg_params q = *p;
+    q.shard_rank = k;
+    q.shard_count = n;
+    return q;
+}
+
+// buffers for a frame of this size (grown, never shrunk)
+int reserve(ptg_multi *m, const ptg_params *p, size_t &slab_elems)
+{
+    const int n = (int)m->shards.size();
     int32_t rows = 0;
-    int rc = ptg_shard_rows(H, BR, n, &rows);
+    int rc = ptg_shard_rows(p->height, p->band_rows, n, &rows);
     if (rc)
         return rc;
-    const size_t slab_elems = (size_t)rows * W * 3, image_elems = (size_t)W * H * 3;
-    std::vector<Device> dv(n);
-    float *gathered = nullptr, *d_image = nullptr;
-    bool comms = false;
-    auto cleanup = [&]() {
-        for (Device &d : dv) {
-            if (d.id < 0)
-                continue;
-            (void)hipSetDevice(d.id);
-            if (d.stream)
-                (void)hipStreamSynchronize(d.stream);
-            if (comms && d.comm)
-                (void)ncclCommDestroy(d.comm);
-            if (d.slab)
-                (void)hipFree(d.slab);
-            if (d.stream)
-                (void)hipStreamDestroy(d.stream);
-            if (d.ctx)
-                (void)ptg_context_destroy(d.ctx);
+    slab_elems = (size_t)rows * p->width * 3;
+    const size_t image_elems = (size_t)p->width * p->height * 3;
+    for (Shard &s : m->shards) {
+        if (s.slab_cap >= slab_elems)
+            continue;
+        MULTI_HIP(hipSetDevice(s.id));
+        if (s.slab) {
+            MULTI_HIP(hipStreamSynchronize(s.stream));
+            MULTI_HIP(hipFree(s.slab));
+            s.slab = nullptr;
+            s.slab_cap = 0;
         }
-        if (n > 0 && dv[0].id >= 0) {
-            (void)hipSetDevice(dv[0].id);
-            if (gathered)
-                (void)hipFree(gathered);
-            if (d_image)
-                (void)hipFree(d_image);
+        if (hipMalloc(&s.slab, slab_elems * sizeof(float)) != hipSuccess)
+            return fail(PTG_ERR_OUT_OF_MEMORY, "multi: hipMalloc of a slab failed");
+        s.slab_cap = slab_elems;
+    }
+    Shard &r = m->shards[0];
+    MULTI_HIP(hipSetDevice(r.id));
+    if (m->gathered_cap < (size_t)n * slab_elems) {
+        MULTI_HIP(hipStreamSynchronize(r.stream));
+        if (m->gathered)
+            MULTI_HIP(hipFree(m->gathered));
+        m->gathered = nullptr;
+        m->gathered_cap = 0;
+        if (hipMalloc(&m->gathered, (size_t)n * slab_elems * sizeof(float)) != hipSuccess)
+            return fail(PTG_ERR_OUT_OF_MEMORY, "multi: hipMalloc of the gather buffer failed");
+        m->gathered_cap = (size_t)n * slab_elems;
+    }
+    if (m->image_cap < image_elems) {
+        MULTI_HIP(hipStreamSynchronize(r.stream));
+        if (m->image)
+            MULTI_HIP(hipFree(m->image));
+        m->image = nullptr;
+        m->image_cap = 0;
+        if (hipMalloc(&m->image, image_elems * sizeof(float)) != hipSuccess)
+            return fail(PTG_ERR_OUT_OF_MEMORY, "multi: hipMalloc of the image failed");
+        m->image_cap = image_elems;
+    }
+    m->host.resize(image_elems);
+    return PTG_OK;
+}
+
+// ONE gather of the equal-size slabs to the root (RCCL: one ncclGather per
+// rank inside a group, rank-major on the root -- rccl.h:745; local shards: the
+// same layout by device copies after each shard's slab is complete), the
+// un-shard there, and the image to the host (m->host).  Synchronous.
+int gather_unshard(ptg_multi *m, const ptg_params *p, size_t slab_elems)
+{
+    const int n = (int)m->shards.size();
+    Shard &root = m->shards[0];
+    if (m->rccl) {
+        ncclResult_t r = ncclGroupStart();
+        if (r != ncclSuccess)
+            return nccl_fail("ncclGroupStart", r);
+        int rc = PTG_OK;
+        for (int k = 0; k < n && rc == PTG_OK; ++k) {
+            Shard &s = m->shards[k];
+            hipError_t e = hipSetDevice(s.id);
+            if (e != hipSuccess) {
+                rc = hip_fail("hipSetDevice", e);
+                break;
+            }
+            r = ncclGather(s.slab, k == 0 ? m->gathered : nullptr, slab_elems, ncclFloat, 0, s.comm, s.stream);
+            if (r != ncclSuccess)
+                rc = nccl_fail("ncclGather", r);
         }
-    };
-#define PTG_MULTI_HIP(call)                                                                             \
-    do {                                                                                                \
-        hipError_t e_ = (call);                                                                         \
-        if (e_ != hipSuccess) {                                                                         \
-            cleanup();                                                                                  \
-            return fail(PTG_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));                \
-        }                                                                                               \
-    } while (0)
-#define PTG_MULTI_NCCL(call)                                                                            \
-    do {                                                                                                \
-        ncclResult_t r_ = (call);                                                                       \
-        if (r_ != ncclSuccess) {                                                                        \
-            cleanup();                                                                                  \
-            return fail(PTG_ERR_HIP, std::string(#call) + ": " + ncclGetErrorString(r_));               \
-        }                                                                                               \
-    } while (0)
-    // per device: the scene in HBM, a stream, the slab; the root also holds
-    // the gathered slabs (rank-major) and the image
-    for (int k = 0; k < n; ++k) {
-        Device &d = dv[k];
-        d.id = devices[k];
-        if ((rc = ptg_context_create(spheres, n_spheres, cam, d.id, &d.ctx))) {
-            cleanup();
+        // the group is closed on every path (an error inside it must not leave
+        // this thread's RCCL group open)
+        r = ncclGroupEnd();
+        if (rc != PTG_OK)
             return rc;
-        }
-        PTG_MULTI_HIP(hipSetDevice(d.id));
-        PTG_MULTI_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-        PTG_MULTI_HIP(hipMalloc(&d.slab, slab_elems * sizeof(float)));
-        if (k == 0) {
-            PTG_MULTI_HIP(hipMalloc(&gathered, (size_t)n * slab_elems * sizeof(float)));
-            PTG_MULTI_HIP(hipMalloc(&d_image, image_elems * sizeof(float)));
+        if (r != ncclSuccess)
+            return nccl_fail("ncclGroupEnd", r);
+        MULTI_HIP(hipSetDevice(root.id));
+    } else {
+        MULTI_HIP(hipSetDevice(root.id));
+        for (int k = 0; k < n; ++k) {
+            Shard &s = m->shards[k];
+            MULTI_HIP(hipEventRecord(s.done, s.stream));
+            MULTI_HIP(hipStreamWaitEvent(root.stream, s.done, 0));
+            MULTI_HIP(hipMemcpyAsync(m->gathered + (size_t)k * slab_elems, s.slab, slab_elems * sizeof(float),
+                                     hipMemcpyDeviceToDevice, root.stream));
         }
     }
-    std::vector<ncclComm_t> cm(n);
-    PTG_MULTI_NCCL(ncclCommInitAll(cm.data(), n, devices));
-    comms = true;
-    for (int k = 0; k < n; ++k)
-        dv[k].comm = cm[k];
+    int rc = ptg_unshard_device(m->gathered, m->image, p->width, p->height, p->band_rows, n, root.stream);
+    if (rc)
+        return rc;
+    const size_t image_elems = (size_t)p->width * p->height * 3;
+    MULTI_HIP(hipMemcpyAsync(m->host.data(), m->image, image_elems * sizeof(float), hipMemcpyDeviceToHost,
+                             root.stream));
+    MULTI_HIP(hipStreamSynchronize(root.stream));
+    // the other shards' streams: their part ended with the gather
+    for (int k = 1; k < n; ++k) {
+        MULTI_HIP(hipSetDevice(m->shards[k].id));
+        MULTI_HIP(hipStreamSynchronize(m->shards[k].stream));
+    }
+    return PTG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptg_multi_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, const int *devices,
+                     int n_devices, ptg_multi **out)
+{
+    return create(spheres, n_spheres, cam, devices, n_devices, true, out);
+}
+
+// internal (tests): n_shards shards on ONE device, gathered by device copies
+// into the same rank-major layout an n-rank ncclGather produces -- the
+// n > 1 slab layout, un-shard and host add of the multi path on a 1-GPU box
+int ptg_multi_create_local_(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int device,
+                            int n_shards, ptg_multi **out)
+{
+    if (n_shards < 1 || n_shards > 64)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi (local): 1 <= n_shards <= 64");
+    std::vector<int> d(n_shards, device);
+    return create(spheres, n_spheres, cam, d.data(), n_shards, false, out);
+}
+
+int ptg_multi_destroy(ptg_multi *m) { return destroy(m); }
+
+int ptg_multi_render(ptg_multi *m, const ptg_params *params, double *image_rgb)
+{
+    int rc = check_frame(m, params);
+    if (rc)
+        return rc;
+    if (!image_rgb)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi: image is NULL");
+    DeviceGuard g;
+    size_t slab_elems = 0;
+    if ((rc = reserve(m, params, slab_elems)))
+        return rc;
+    const int n = (int)m->shards.size();
     // the shards render concurrently (asynchronous launches on each device)
     for (int k = 0; k < n; ++k) {
-        ptg_params p = *params;
-        p.shard_rank = k;
-        p.shard_count = n;
-        if ((rc = ptg_render_device(dv[k].ctx, &p, dv[k].slab, nullptr, dv[k].stream))) {
-            cleanup();
+        const ptg_params q = shard_params(params, k, n);
+        if ((rc = ptg_render_device(m->shards[k].ctx, &q, m->shards[k].slab, nullptr, m->shards[k].stream)))
             return rc;
-        }
     }
-    // ONE gather of equal-size slabs to the first device, fused across the
-    // process's ranks in a group
-    PTG_MULTI_NCCL(ncclGroupStart());
-    for (int k = 0; k < n; ++k) {
-        PTG_MULTI_HIP(hipSetDevice(dv[k].id));
-        PTG_MULTI_NCCL(ncclGather(dv[k].slab, k == 0 ? gathered : nullptr, slab_elems, ncclFloat, 0, dv[k].comm,
-                                  dv[k].stream));
-    }
-    PTG_MULTI_NCCL(ncclGroupEnd());
-    PTG_MULTI_HIP(hipSetDevice(dv[0].id));
-    if ((rc = ptg_unshard_device(gathered, d_image, W, H, BR, n, dv[0].stream))) {
-        cleanup();
+    if ((rc = gather_unshard(m, params, slab_elems)))
         return rc;
-    }
-    std::vector<float> host(image_elems);
-    PTG_MULTI_HIP(hipMemcpyAsync(host.data(), d_image, image_elems * sizeof(float), hipMemcpyDeviceToHost,
-                                 dv[0].stream));
-    PTG_MULTI_HIP(hipStreamSynchronize(dv[0].stream));
+    const size_t image_elems = (size_t)params->width * params->height * 3;
     for (size_t i = 0; i < image_elems; ++i)
-        image_rgb[i] = image_rgb[i] + (double)host[i];  // main.cpp:196: image[row] += ...
-    cleanup();
+        image_rgb[i] = image_rgb[i] + (double)m->host[i];  // main.cpp:196: image[row] += ...
     return PTG_OK;
-#undef PTG_MULTI_HIP
-#undef PTG_MULTI_NCCL
 }
+
+int ptg_multi_reset_accumulation(ptg_multi *m, const ptg_params *params)
+{
+    int rc = check_frame(m, params);
+    if (rc)
+        return rc;
+    DeviceGuard g;
+    const int n = (int)m->shards.size();
+    for (int k = 0; k < n; ++k) {
+        const ptg_params q = shard_params(params, k, n);
+        if ((rc = ptg_reset_accumulation_device(m->shards[k].ctx, &q, m->shards[k].stream)))
+            return rc;
+    }
+    return PTG_OK;
+}
+
+int ptg_multi_accumulate(ptg_multi *m, const ptg_params *params, int32_t sample_begin, int32_t sample_end)
+{
+    int rc = check_frame(m, params);
+    if (rc)
+        return rc;
+    DeviceGuard g;
+    const int n = (int)m->shards.size();
+    for (int k = 0; k < n; ++k) {
+        const ptg_params q = shard_params(params, k, n);
+        if ((rc = ptg_accumulate_device(m->shards[k].ctx, &q, sample_begin, sample_end, nullptr,
+                                        m->shards[k].stream)))
+            return rc;
+    }
+    return PTG_OK;
+}
+
+int ptg_multi_resolve(ptg_multi *m, const ptg_params *params, int32_t samples_done, float *image_rgb)
+{
+    int rc = check_frame(m, params);
+    if (rc)
+        return rc;
+    if (!image_rgb)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_resolve: image is NULL");
+    DeviceGuard g;
+    size_t slab_elems = 0;
+    if ((rc = reserve(m, params, slab_elems)))
+        return rc;
+    const int n = (int)m->shards.size();
+    for (int k = 0; k < n; ++k) {
+        const ptg_params q = shard_params(params, k, n);
+        if ((rc = ptg_resolve_device(m->shards[k].ctx, &q, samples_done, m->shards[k].slab, m->shards[k].stream)))
+            return rc;
+    }
+    if ((rc = gather_unshard(m, params, slab_elems)))
+        return rc;
+    const size_t image_elems = (size_t)params->width * params->height * 3;
+    std::copy(m->host.begin(), m->host.begin() + image_elems, image_rgb);
+    return PTG_OK;
+}
+
+int ptg_render_multi(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, const ptg_params *params,
+                     const int *devices, int n_devices, double *image_rgb)
+{
+    if (!params || !image_rgb || !devices || n_devices < 1)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi: NULL argument or no device");
+    ptg_multi probe;  // argument checks before any device work
+    probe.shards.resize(1);
+    int rc = check_frame(&probe, params);
+    if (rc)
+        return rc;
+    ptg_multi *m = nullptr;
+    if ((rc = ptg_multi_create(spheres, n_spheres, cam, devices, n_devices, &m)))
+        return rc;
+    rc = ptg_multi_render(m, params, image_rgb);
+    ptg_multi_destroy(m);
+    return rc;
+}
+
+}  // extern "C"

@@ -68,6 +68,10 @@ int fail(int code, const std::string &msg)
 #endif
 constexpr int kBlock = PTG_BLOCK;
 constexpr int kMaxLevels = 4;     // unit levels: head + up to 3 split-tail levels
+// samples per sub-pixel in one work unit, at most: a unit's paths are indexed
+// it < 64 * chunk <= 2^22, where render_kernel's float-reciprocal divmod_nv is
+// exact (fill_launch caps every level's chunk)
+constexpr int kMaxChunk = 1 << 16;
 constexpr int kTraceBlock = 256;  // parity probe kernel
 #ifndef PTG_MAX_LDS_SPHERES
 #define PTG_MAX_LDS_SPHERES 64
@@ -1348,8 +1352,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             return lds_pre[wv][lane];
         }
     };
-    // it / nv and it % nv (it < 2^24, only for a unit of fewer than 64
-    // slots) through a float reciprocal formed at each use: the compiler's
+    // it / nv and it % nv (only for a unit of fewer than 64 slots; it <
+    // 64 * kMaxChunk = 2^22, so the float quotient is within 1 of it / nv and
+    // one correction step is exact) through a float reciprocal formed at
+    // each use: the compiler's
     // integer division by the unit's nv kept its constants in VGPRs for the
     // whole unit (spilled to scratch)
     auto divmod_nv = [&](int it, int &q, int &r) {
@@ -2204,7 +2210,7 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     const long long tail_min = (long long)(ctx->n > kLinearMax ? PTG_BVH_TAIL_MIN_HALF_ROUNDS : PTG_TAIL_MIN_HALF_ROUNDS) *
                                ctx->wave_slots / 2;
     const bool tail_ok = p->chunk_samples <= 0 && !accumulate_only && s_begin == 0 && s_end == p->samples &&
-                         PTG_TAIL_CHUNKS > 1 && nsamp >= PTG_TAIL_CHUNKS && groups >= tail_min;
+                         PTG_TAIL_CHUNKS > 1 && nsamp >= PTG_TAIL_CHUNKS && nsamp <= kMaxChunk && groups >= tail_min;
     int chunk = p->chunk_samples;
     if (tail_ok) {
         chunk = nsamp;
@@ -2216,6 +2222,8 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     }
     if (chunk > nsamp)
         chunk = nsamp > 0 ? nsamp : 1;
+    if (chunk > kMaxChunk)  // the kernel's divmod_nv needs 64 * chunk <= 2^22 (the image does not depend on it)
+        chunk = kMaxChunk;
     A.chunk = chunk;
     A.n_groups = groups;
     int n_chunks = nsamp > 0 ? (nsamp + chunk - 1) / chunk : 0;

@@ -19,7 +19,8 @@ EXPORTS = (
     "ptg_context_create", "ptg_context_destroy", "ptg_shard_rows", "ptg_render_device",
     "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
     "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device", "ptg_scene_layout",
-    "ptg_render_multi",
+    "ptg_render_multi", "ptg_multi_create", "ptg_multi_destroy", "ptg_multi_render",
+    "ptg_multi_reset_accumulation", "ptg_multi_accumulate", "ptg_multi_resolve",
 )
 
 
@@ -65,6 +66,14 @@ def lib():
             "ptg_resolve_device": (I, [P, C.POINTER(Params), C.c_int32, P, P]),
             "ptg_scene_layout": (I, [P, C.c_size_t, P, P, P]),
             "ptg_render_multi": (I, [P, C.c_size_t, P, C.POINTER(Params), C.POINTER(C.c_int), I, P]),
+            "ptg_multi_create": (I, [P, C.c_size_t, P, C.POINTER(C.c_int), I, C.POINTER(C.c_void_p)]),
+            "ptg_multi_destroy": (I, [P]),
+            "ptg_multi_render": (I, [P, C.POINTER(Params), P]),
+            "ptg_multi_reset_accumulation": (I, [P, C.POINTER(Params)]),
+            "ptg_multi_accumulate": (I, [P, C.POINTER(Params), C.c_int32, C.c_int32]),
+            "ptg_multi_resolve": (I, [P, C.POINTER(Params), C.c_int32, P]),
+            # internal (tests): n shards on one device, gathered by device copies
+            "ptg_multi_create_local_": (I, [P, C.c_size_t, P, I, I, C.POINTER(C.c_void_p)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

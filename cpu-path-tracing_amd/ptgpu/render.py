@@ -118,6 +118,71 @@ def render_multi(scn, cam, image: np.ndarray, width: int, height: int, samples: 
     return image
 
 
+class MultiContext:
+    """A persistent multi-GPU context (ptg_multi): the scene on every device,
+    the RCCL communicator of the device set, the root's gather buffers --
+    repeated frames and progressive passes reuse them.  `local_shards=n`
+    (tests) puts n shards on the one device `devices[0]`, gathered by device
+    copies into the layout an n-rank ncclGather produces."""
+
+    def __init__(self, scn, cam, devices, local_shards: int = 0):
+        sp = _spheres_array(scn)
+        ca = _camera_array(cam)
+        h = C.c_void_p()
+        if local_shards:
+            check(lib().ptg_multi_create_local_(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p),
+                                                int(devices[0]), int(local_shards), C.byref(h)),
+                  "ptg_multi_create_local_")
+        else:
+            devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+            check(lib().ptg_multi_create(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), devs,
+                                         len(devices), C.byref(h)), "ptg_multi_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().ptg_multi_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def _image(image, params, dtype):
+        if image.dtype != dtype or not image.flags["C_CONTIGUOUS"] or \
+                image.size != params.width * params.height * 3:
+            raise ValueError(f"image must be a C-contiguous {np.dtype(dtype).name} array of width*height*3 values")
+        return image.ctypes.data_as(C.c_void_p)
+
+    def render(self, image: np.ndarray, params: Params) -> np.ndarray:
+        """The frame over all devices, added into `image` (float64, like render())."""
+        check(lib().ptg_multi_render(self._h, C.byref(params), self._image(image, params, np.float64)),
+              "ptg_multi_render")
+        return image
+
+    def reset_accumulation(self, params: Params) -> None:
+        check(lib().ptg_multi_reset_accumulation(self._h, C.byref(params)), "ptg_multi_reset_accumulation")
+
+    def accumulate(self, params: Params, sample_begin: int, sample_end: int) -> None:
+        check(lib().ptg_multi_accumulate(self._h, C.byref(params), int(sample_begin), int(sample_end)),
+              "ptg_multi_accumulate")
+
+    def resolve(self, image: np.ndarray, params: Params, samples_done: int) -> np.ndarray:
+        """The image of the samples accumulated so far, written to `image` (float32)."""
+        check(lib().ptg_multi_resolve(self._h, C.byref(params), int(samples_done),
+                                      self._image(image, params, np.float32)), "ptg_multi_resolve")
+        return image
+
+
 def scene_layout(scn, cam):
     """Host-side scene preparation (ptg_scene_layout, no device needed): the
     anchor axis of each huge sphere (-1: camera-facing anchor, or not huge)

@@ -127,9 +127,34 @@ int ptg_render(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *ca
  * b % n_devices == k (band_rows from params), ONE ncclGather (RCCL over xGMI,
  * rccl.h:745) collects the slabs on devices[0], which un-shards the frame.
  * The image equals ptg_render's bit for bit (the RNG is keyed by the global
- * pixel).  Replaces main.cpp:214-236 for a caller owning several GPUs. */
+ * pixel).  Replaces main.cpp:214-236 for a caller owning several GPUs.
+ * fp32 kernel only: PTG_FLAG_REFERENCE_F64 is refused (PTG_ERR_UNSUPPORTED;
+ * ptg_render keeps that mode's doubles).  The caller's current HIP device is
+ * restored on return.  ptg_render_multi = ptg_multi_create + ptg_multi_render
+ * + ptg_multi_destroy. */
 int ptg_render_multi(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam,
                      const ptg_params *params, const int *devices, int n_devices, double *image_rgb);
+
+/* A persistent multi-GPU context: per device the scene in HBM, a stream and
+ * the slab, the RCCL communicator of the device set (ncclCommInitAll once),
+ * the root's gather buffer and image -- repeated and progressive frames
+ * reuse them.  Not re-entrant. */
+typedef struct ptg_multi ptg_multi;
+int ptg_multi_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, const int *devices,
+                     int n_devices, ptg_multi **out);
+int ptg_multi_destroy(ptg_multi *m);
+/* ptg_render_multi's frame on the context (synchronous; adds into image_rgb
+ * like main.cpp:196). */
+int ptg_multi_render(ptg_multi *m, const ptg_params *params, double *image_rgb);
+/* Progressive passes over all devices (README.md:9): reset, then sample
+ * passes [begin, end) queued on every device (asynchronous), then a resolve
+ * of the samples so far -- each device resolves its bands, ONE gather, the
+ * un-shard -- written (not added) to image_rgb as W*H*3 floats in the
+ * reference's row order (synchronous).  After passes covering [0, samples)
+ * the resolve equals ptg_render's image bit for bit. */
+int ptg_multi_reset_accumulation(ptg_multi *m, const ptg_params *params);
+int ptg_multi_accumulate(ptg_multi *m, const ptg_params *params, int32_t sample_begin, int32_t sample_end);
+int ptg_multi_resolve(ptg_multi *m, const ptg_params *params, int32_t samples_done, float *image_rgb);
 
 /* ---- device-resident path (bench, multi-GPU) --------------------------
  * A context holds the prepared scene in HBM on one device. */

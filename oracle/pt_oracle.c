@@ -803,6 +803,16 @@ static void box_mode_B(const po_sphere *s, int n, const po_camera *cam, const bo
     }
 }
 
+/* sphB array + a compact copy of the lex scan's hot fields behind it: per
+ * sphere {P, -R^2} (NaN for huge spheres: never rejected early), 16 B, so a
+ * 10,000-sphere scan streams 160 KB instead of the whole records */
+static sphB *malloc_sphB(int n)
+{
+    const size_t m = (size_t)(n > 0 ? n : 1);
+    return (sphB *)malloc(sizeof(sphB) * m + 4 * sizeof(float) * m);
+}
+static float *hot_B(const sphB *s, int n) { return (float *)(s + (n > 0 ? n : 1)); }
+
 static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, camB *cb)
 {
     boxB box = scene_box_B(s, n, cam);
@@ -882,6 +892,13 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
     trig_table_B(cb->trig);
     cb->invW = 0.0f;
     cb->invH = 0.0f;
+    float *hot = hot_B(out, n);
+    for (int i = 0; i < n; ++i) {
+        hot[4 * i + 0] = out[i].P.x;
+        hot[4 * i + 1] = out[i].P.y;
+        hot[4 * i + 2] = out[i].P.z;
+        hot[4 * i + 3] = out[i].big ? NAN : out[i].negR2;
+    }
 }
 
 /* sin/cos of 2*pi*u, u = m * 2^-24 with m the draw's 24-bit integer (replaces
@@ -1116,61 +1133,99 @@ static int intersect_B(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout
  * smallest t wins, lowest index on ties (main.cpp:35 strict < in index order).
  * Per-sphere arithmetic as intersect_B; the cull compares against tb. */
 #define LINEAR_MAX 64
+/* The discriminant of sphere sp (the kernel's forms; hb, c as above). */
+static float disc_B_lex(const sphB *sp, f3 e, f3 d, float a, float hb, float c)
+{
+    float disc = fmaf(hb, hb, -(a * c));
+    if (!sp->big && !(g_bvar & PO_BV_DISC_NAIVE)) {
+        /* Lagrange form, limited to hb^2 for an origin outside (c >= 0:
+         * exactly disc <= hb^2) so that the cull below stays exact */
+        f3 x = fcross(e, d);
+        disc = fmaf(a, -sp->negR2, -fdot(x, x));
+        disc = c >= 0.0f ? fminf(disc, hb * hb) : disc;
+    }
+    return disc;
+}
+
 static int intersect_B_lex(const sphB *s, int n, f3 o, f3 d, float *tout, int *idout)
 {
     float a = fdot(d, d);
     float tb = INFF;
     int id = -1;
-    for (int i = 0; i < n; ++i) {
-        const sphB *sp = &s[i];
-        f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
-        float ed = fdot(e, d);
-        float ee = fdot(e, e);
-        float hb, c;
-        if (sp->big) {
-            hb = fmaf(sp->R, fdot(sp->N, d), ed);
-            c = fmaf(sp->R2x, fdot(e, sp->N), ee);
-        } else {
-            hb = ed;
-            c = ee + sp->negR2;
+    /* Blocks of 64 spheres: first the rejections that do not depend on tb
+     * (both roots behind, no real root: the same disc as below), branch-free
+     * from a compact copy of the records, then the full test of the
+     * survivors in index order.  Every rejection is a pure "skip", so the
+     * result is that of testing every sphere in order (only faster: the
+     * unpredictable branches ran for all 10,000 spheres of C5). */
+    const float *hot = hot_B(s, n);
+    const int naive = (g_bvar & PO_BV_DISC_NAIVE) != 0;
+    int cand[64];
+    for (int b0 = 0; b0 < n; b0 += 64) {
+        const int b1 = b0 + 64 < n ? b0 + 64 : n;
+        int nc = 0;
+        for (int i = b0; i < b1; ++i) {
+            const float *h = hot + 4 * i;
+            const f3 e = fk(o.x - h[0], o.y - h[1], o.z - h[2]);
+            const float hb = fdot(e, d), c = fdot(e, e) + h[3];  /* huge spheres: NaN, kept */
+            float disc;
+            if (naive) {
+                disc = fmaf(hb, hb, -(a * c));
+            } else {
+                const f3 x = fcross(e, d);
+                disc = fmaf(a, -h[3], -fdot(x, x));
+                /* = fminf(disc, m) (NaN operands included) without the libm call */
+                const float m = hb * hb;
+                disc = c >= 0.0f ? (disc < m ? disc : (m != m ? disc : m)) : disc;
+            }
+            cand[nc] = i;
+            nc += !((hb >= 0.0f) & (c >= 0.0f)) & !(disc < 0.0f);
         }
-        if (hb >= 0.0f && c >= 0.0f)
-            continue;
-        if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * CULL_MARGIN)
-            continue;
-        float disc = fmaf(hb, hb, -(a * c));
-        if (!sp->big && !(g_bvar & PO_BV_DISC_NAIVE)) {
-            /* Lagrange form, limited to hb^2 for an origin outside (c >= 0:
-             * exactly disc <= hb^2) so that the cull above stays exact */
-            f3 x = fcross(e, d);
-            disc = fmaf(a, -sp->negR2, -fdot(x, x));
-            disc = c >= 0.0f ? fminf(disc, hb * hb) : disc;
-        }
-        if (disc < 0.0f)
-            continue;
-        float sq = sqrt_scan_B(disc);
-        float num, den;
-        if (hb < 0.0f) {
-            float q = sq - hb;
-            num = c;
-            den = q;
-            if (c < EPSF * q) {
-                num = q;
-                den = a;
-                if (q < EPSF * a)
+        for (int k = 0; k < nc; ++k) {
+            const int i = cand[k];
+            const sphB *sp = &s[i];
+            f3 e = fk(o.x - sp->P.x, o.y - sp->P.y, o.z - sp->P.z);
+            float ed = fdot(e, d);
+            float ee = fdot(e, e);
+            float hb, c;
+            if (sp->big) {
+                hb = fmaf(sp->R, fdot(sp->N, d), ed);
+                c = fmaf(sp->R2x, fdot(e, sp->N), ee);
+            } else {
+                hb = ed;
+                c = ee + sp->negR2;
+            }
+            if (hb >= 0.0f && c >= 0.0f)
+                continue;
+            if (hb < 0.0f && c > 0.0f && c >= (tb * (-2.0f * hb)) * CULL_MARGIN)
+                continue;
+            float disc = disc_B_lex(sp, e, d, a, hb, c);
+            if (disc < 0.0f)
+                continue;
+            float sq = sqrt_scan_B(disc);
+            float num, den;
+            if (hb < 0.0f) {
+                float q = sq - hb;
+                num = c;
+                den = q;
+                if (c < EPSF * q) {
+                    num = q;
+                    den = a;
+                    if (q < EPSF * a)
+                        continue;
+                }
+            } else {
+                float qn = hb + sq;
+                num = -c;
+                den = qn;
+                if (num < EPSF * den)
                     continue;
             }
-        } else {
-            float qn = hb + sq;
-            num = -c;
-            den = qn;
-            if (num < EPSF * den)
-                continue;
-        }
-        float t = num / den;
-        if (t < tb) {
-            tb = t;
-            id = i;
+            float t = num / den;
+            if (t < tb) {
+                tb = t;
+                id = i;
+            }
         }
     }
     *tout = tb;
@@ -1343,7 +1398,7 @@ int po_render_xs_f32_ex(const po_sphere *s, int n, const po_camera *cam, int W, 
 {
     if (check_args(n, W, H, samps, nsub) || ystep <= 0)
         return -1;
-    sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
+    sphB *sb = malloc_sphB(n);
     camB cb;
     prep_B(s, n, cam, sb, &cb);
     cb.invW = 1.0f / (float)W;
@@ -1379,6 +1434,80 @@ int po_render_xs_f32_ex(const po_sphere *s, int n, const po_camera *cam, int W, 
     return 0;
 }
 
+/* Rectangle renders (tests at the BASELINE sample counts): pixels
+ * x in [x0, x1) of rows y = y0, y0 + ystep, ... < y1, parallel over PIXELS
+ * (the row renders above are parallel over rows, so one row runs on one
+ * thread).  Same per-pixel arithmetic as po_render_xs_f64 / _f32; pixels
+ * outside the rectangle are left untouched. */
+int po_render_xs_f64_rect(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                          uint64_t seed, int x0, int x1, int y0, int y1, int ystep, int nthreads, double *image,
+                          uint64_t *segments)
+{
+    if (check_args(n, W, H, samps, nsub) || ystep <= 0 || x0 < 0 || x1 > W || x0 > x1 || y0 < 0 || y1 > H)
+        return -1;
+    const long nx = x1 - x0, ny = y1 > y0 ? (y1 - y0 + ystep - 1) / ystep : 0;
+    uint64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+    for (long i = 0; i < nx * ny; ++i) {
+        const int y = y0 + (int)(i / nx) * ystep, x = x0 + (int)(i % nx);
+        for (int sy = 0; sy < nsub; ++sy)
+            for (int sx = 0; sx < nsub; ++sx) {
+                uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) +
+                              (uint64_t)(sy * nsub + sx);
+                rngA r = {NULL, 0, 0};
+                uint64_t segs = 0;
+                v3 a = subpixel_A(s, n, cam, W, H, samps, nsub, x, y, sx, sy, &r, po_key_hash(seed, ps), &segs);
+                total += segs;
+                double *px = image + 3 * ((size_t)(H - y - 1) * (size_t)W + (size_t)x);
+                double q = 1.0 / (nsub * nsub);
+                px[0] = px[0] + po_clamp(a.x) * q;
+                px[1] = px[1] + po_clamp(a.y) * q;
+                px[2] = px[2] + po_clamp(a.z) * q;
+            }
+    }
+    if (segments)
+        *segments = total;
+    return 0;
+}
+
+int po_render_xs_f32_rect(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                          uint64_t seed, int x0, int x1, int y0, int y1, int ystep, int nthreads, float *image,
+                          uint64_t *segments)
+{
+    if (check_args(n, W, H, samps, nsub) || ystep <= 0 || x0 < 0 || x1 > W || x0 > x1 || y0 < 0 || y1 > H)
+        return -1;
+    sphB *sb = malloc_sphB(n);
+    camB cb;
+    prep_B(s, n, cam, sb, &cb);
+    cb.invW = 1.0f / (float)W;
+    cb.invH = 1.0f / (float)H;
+    const long nx = x1 - x0, ny = y1 > y0 ? (y1 - y0 + ystep - 1) / ystep : 0;
+    uint64_t total = 0;
+    float q = 1.0f / (float)(nsub * nsub);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+    for (long i = 0; i < nx * ny; ++i) {
+        const int y = y0 + (int)(i / nx) * ystep, x = x0 + (int)(i % nx);
+        f3 pix = fk(0, 0, 0);
+        for (int sy = 0; sy < nsub; ++sy)
+            for (int sx = 0; sx < nsub; ++sx) {
+                uint64_t ps = ((uint64_t)y * (uint64_t)W + (uint64_t)x) * (uint64_t)(nsub * nsub) +
+                              (uint64_t)(sy * nsub + sx);
+                uint64_t segs = 0, bad = 0;
+                f3 a = subpixel_B(sb, n, &cb, samps, nsub, x, y, sx, sy, po_key_hash(seed, ps), &segs, &bad);
+                total += segs;
+                pix = fk(fmaf(clampf_B(a.x), q, pix.x), fmaf(clampf_B(a.y), q, pix.y), fmaf(clampf_B(a.z), q, pix.z));
+            }
+        const size_t row = (size_t)(H - y - 1) * (size_t)W + (size_t)x;
+        image[3 * row + 0] = pix.x;
+        image[3 * row + 1] = pix.y;
+        image[3 * row + 2] = pix.z;
+    }
+    free(sb);
+    if (segments)
+        *segments = total;
+    return 0;
+}
+
 void po_mode_b_math(const float *a, const float *b, size_t n, float *quot, float *root)
 {
     for (size_t i = 0; i < n; ++i) {
@@ -1407,7 +1536,7 @@ int po_scan_layout(const po_sphere *s, int n, const po_camera *cam, int32_t *axi
 {
     if (n < 0)
         return -1;
-    sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
+    sphB *sb = malloc_sphB(n);
     camB cb;
     prep_B(s, n, cam, sb, &cb);
     for (int i = 0; i < n; ++i) {
@@ -1421,7 +1550,7 @@ int po_scan_layout(const po_sphere *s, int n, const po_camera *cam, int32_t *axi
 int po_sample_f32(const po_sphere *s, int n, const po_camera *cam, int W, int H, int nsub, uint64_t seed, int x,
                   int y, int sx, int sy, uint32_t sample, float out[3])
 {
-    sphB *sb = (sphB *)malloc(sizeof(sphB) * (size_t)(n > 0 ? n : 1));
+    sphB *sb = malloc_sphB(n);
     camB cb;
     prep_B(s, n, cam, sb, &cb);
     cb.invW = 1.0f / (float)W;

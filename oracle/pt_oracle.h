@@ -144,6 +144,14 @@ int po_render_xs_f32(const po_sphere *s, int n, const po_camera *cam, int W, int
 int po_render_xs_f32_ex(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
                         uint64_t seed, int y0, int y1, int ystep, int nthreads, float *image, uint64_t *segments,
                         uint64_t *out_of_range);
+/* The same for the pixels x in [x0, x1) of rows y0, y0 + ystep, ... < y1,
+ * parallel over pixels (for single rows at large sample counts). */
+int po_render_xs_f64_rect(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                          uint64_t seed, int x0, int x1, int y0, int y1, int ystep, int nthreads, double *image,
+                          uint64_t *segments);
+int po_render_xs_f32_rect(const po_sphere *s, int n, const po_camera *cam, int W, int H, int samps, int nsub,
+                          uint64_t seed, int x0, int x1, int y0, int y1, int ystep, int nthreads, float *image,
+                          uint64_t *segments);
 /* One Mode-B path for a given (pixel, sub, sample): returns radiance and
  * segment count -- used by the per-sample GPU parity test. */
 /* Mode B arithmetic primitives: quot[i] = div_B(a[i], b[i]) (b > 0),

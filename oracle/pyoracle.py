@@ -71,6 +71,8 @@ def lib():
             "po_render_xs_f64": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P]),
             "po_render_xs_f32": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P]),
             "po_render_xs_f32_ex": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, P, P, P]),
+            "po_render_xs_f64_rect": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, I, I, P, P]),
+            "po_render_xs_f32_rect": (I, [P, I, P, I, I, I, I, U64, I, I, I, I, I, I, P, P]),
             "po_sample_f32": (I, [P, I, P, I, I, I, U64, I, I, I, I, U32, P]),
             "po_tonemap": (None, [P, C.c_size_t, P]),
             "po_scan_layout": (I, [P, I, P, P, P]),
@@ -183,6 +185,22 @@ def render_xs_f32(spheres, cam, W, H, samps, nsub=2, seed=0x5EED0001, rows=None,
     segs = np.zeros(1, dtype=np.uint64)
     rc = lib().po_render_xs_f32(ptr(spheres), len(spheres), ptr(cam), W, H, samps, nsub, seed,
                                 y0, y1, ys, nthreads, ptr(img), ptr(segs))
+    assert rc == 0
+    return img.reshape(H, W, 3), int(segs[0])
+
+
+def render_xs_rect(spheres, cam, W, H, samps, nsub=2, seed=0x5EED0001, cols=None, rows=None, nthreads=8,
+                   f64=False):
+    """Mode A/xs (f64=True) or Mode B image of the pixels x in cols = (x0, x1)
+    of rows = (y0, y1, ystep), rendered in parallel over pixels (a single row
+    at a large sample count uses every thread); other pixels stay 0."""
+    x0, x1 = cols if cols is not None else (0, W)
+    y0, y1, ys = rows if rows is not None else (0, H, 1)
+    img = np.zeros((H * W * 3,), dtype=np.float64 if f64 else np.float32)
+    segs = np.zeros(1, dtype=np.uint64)
+    fn = lib().po_render_xs_f64_rect if f64 else lib().po_render_xs_f32_rect
+    rc = fn(ptr(spheres), len(spheres), ptr(cam), W, H, samps, nsub, seed, x0, x1, y0, y1, ys, nthreads, ptr(img),
+            ptr(segs))
     assert rc == 0
     return img.reshape(H, W, 3), int(segs[0])
 

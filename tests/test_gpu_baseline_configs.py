@@ -1,0 +1,133 @@
+"""C4 and C5 at their BASELINE.json sample counts (VERDICT r2 "what's missing" 1).
+
+C4 = box_scene 3840x2160 at 4096 spp (1024 samples per sub-pixel), tile-sharded
+over 8 GPUs; C5 = the synthetic 10,000-sphere scene at 1920x1080, 1024 spp.
+Their launch shape (unit levels, split tail, BVH head/tail chunks) depends on
+the sample count, so they are rendered here at the full count:
+
+* C4: the whole frame on one GPU and as 8 interleaved row-band shards
+  gathered and un-sharded on the device -- bit-equal; rows of the head and of
+  the split tail bit-exact against the oracle's Mode B (the kernel's fp32 op
+  sequence) and within the north star's per-pixel RMSE < 1e-3 of Mode A/xs
+  (the reference's double arithmetic, line by line, same counter-RNG draws).
+* C5: a head row in the sphere field (y = 300) and a split-tail row (y = 2),
+  each in two halves (one test each: the double oracle scans all 10,000
+  spheres, ~25 s per half row on 16 threads), bit-exact vs Mode B and RMSE <
+  1e-3 vs Mode A/xs.  (Round 2 checked C5 only at 64 spp, where the fp32
+  floor is 1.1e-3.)
+
+The oracle renders these rows in parallel over pixels (po_render_xs_*_rect).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ptgpu  # noqa: E402
+import pyoracle as po  # noqa: E402
+
+SEED = 0x5EED0001
+NORTH_STAR_RMSE = 1e-3
+NT = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
+_cache = {}
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a visible MI355X")
+
+
+def _arrays(scn):
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    return (cam, np.ascontiguousarray(scn.to_array().view(po.SPHERE_DT)),
+            np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT)))
+
+
+def _frame(name, W, H, samps, shards=1):
+    """The frame on one GPU (shards = 1) or as `shards` interleaved single-row
+    band slabs gathered rank-major and un-sharded on the device."""
+    key = (name, W, H, samps, shards)
+    if key not in _cache:
+        scn = ptgpu.make_scene(name, W, H)
+        cam, _, _ = _arrays(scn)
+        rows = ptgpu.shard_rows(H, 1, shards)
+        gathered = torch.full((shards, rows * W * 3), -7.0, dtype=torch.float32, device="cuda")
+        with ptgpu.Context(scn, cam) as ctx:
+            for k in range(shards):
+                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, shards))
+            image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+            ptgpu.unshard_device(gathered, image, W, H, 1, shards)
+            torch.cuda.synchronize()
+        _cache[key] = image.cpu().numpy()
+        del gathered, image
+    return _cache[key]
+
+
+def _rows_vs_oracle(name, W, H, samps, gpu, y, cols):
+    """Row y (image space, main.cpp:181: y = 0 at the bottom), pixels cols:
+    bit-exact vs Mode B; returns the squared errors vs Mode A/xs."""
+    scn = ptgpu.make_scene(name, W, H)
+    _, sp, ca = _arrays(scn)
+    x0, x1 = cols
+    b, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, cols=cols, rows=(y, y + 1, 1), nthreads=NT)
+    g = gpu[H - 1 - y, x0:x1]
+    bb = b[H - 1 - y, x0:x1]
+    diff = np.abs(g.astype(np.float64) - bb.astype(np.float64))
+    assert float(diff.max()) == 0.0, (y, float(diff.max()), int((diff > 0).sum()))
+    a, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, cols=cols, rows=(y, y + 1, 1), nthreads=NT, f64=True)
+    return (g.astype(np.float64) - a[H - 1 - y, x0:x1]) ** 2
+
+
+C4 = ("box", 3840, 2160, 1024)  # BASELINE configs[3]: 4096 spp = 1024 samples per sub-pixel
+C5 = ("synthetic:10000", 1920, 1080, 256)  # configs[4]: 1024 spp
+
+
+def test_c4_full_spp_eight_shards_equal_the_frame():
+    _require_gpu()
+    full = _frame(*C4)
+    sharded = _frame(*C4, shards=8)
+    assert np.array_equal(full, sharded)
+    assert full.min() >= 0.0 and full.max() <= 1.0 and full.mean() > 0.05
+
+
+# y = 0, 1: the last slab rows (the split tail of the one-GPU frame and of each
+# 8-way shard); 1337, H - 1: head rows
+@pytest.mark.parametrize("y", [0, 1, 1337, 2159])
+def test_c4_full_spp_rows_vs_oracle(y):
+    _require_gpu()
+    name, W, H, samps = C4
+    sq = _rows_vs_oracle(name, W, H, samps, _frame(*C4), y, (0, W))
+    rmse = float(np.sqrt(sq.mean()))
+    assert rmse < NORTH_STAR_RMSE, (y, rmse)
+    _cache.setdefault("c4_sq", []).append(sq)
+
+
+def test_c4_full_spp_rmse_over_rows():
+    sq = _cache.get("c4_sq")
+    if not sq:
+        pytest.skip("needs test_c4_full_spp_rows_vs_oracle")
+    rmse = float(np.sqrt(np.concatenate([s.reshape(-1) for s in sq]).mean()))
+    assert rmse < NORTH_STAR_RMSE, rmse
+
+
+# y = 300: head row across the sphere field; y = 2: a split-tail row (the BVH
+# frame's last ~69 slab rows); each row in two halves
+@pytest.mark.parametrize("y,cols", [(300, (0, 960)), (300, (960, 1920)), (2, (0, 960)), (2, (960, 1920))])
+def test_c5_full_spp_rows_vs_oracle(y, cols):
+    _require_gpu()
+    name, W, H, samps = C5
+    sq = _rows_vs_oracle(name, W, H, samps, _frame(*C5), y, cols)
+    rmse = float(np.sqrt(sq.mean()))
+    assert rmse < NORTH_STAR_RMSE, (y, cols, rmse)
+    _cache.setdefault("c5_sq", []).append(sq)
+
+
+def test_c5_full_spp_rmse_over_rows():
+    sq = _cache.get("c5_sq")
+    if not sq:
+        pytest.skip("needs test_c5_full_spp_rows_vs_oracle")
+    rmse = float(np.sqrt(np.concatenate([s.reshape(-1) for s in sq]).mean()))
+    assert rmse < NORTH_STAR_RMSE, rmse

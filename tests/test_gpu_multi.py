@@ -1,0 +1,121 @@
+"""Multi-GPU contexts of one process (VERDICT r2 next 2,
+ADVICE r2): the persistent ptg_multi context -- repeated frames and
+progressive passes without re-creating the RCCL communicator or the scenes --
+and the n > 1 slab layout of its gather.
+
+On the 1-GPU test box the RCCL path runs as a one-rank communicator; the
+n-rank layout (rank-major slabs on the root, un-shard, host add) runs with n
+shards on the one device (ptg_multi_create_local_: the same code, the gather
+done by device copies into the layout an n-rank ncclGather produces).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ptgpu  # noqa: E402
+import pyoracle as po  # noqa: E402
+
+SEED = 0x5EED0001
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a visible MI355X")
+
+
+def _ref(scn, cam, W, H, samps):
+    img = np.zeros((H * W, 3))
+    ptgpu.render(scn, cam, img, W, H, samps)
+    return img
+
+
+@pytest.mark.parametrize("local", [0, 2, 3, 8])
+def test_multi_context_frames_and_progressive_passes(local):
+    """A persistent context: two frames add into the image like ptg_render
+    (image[row] += ..., main.cpp:196), frames of another size reuse it, and
+    progressive passes over all shards resolve to the one-shot image bit for
+    bit (previews equal the oracle at that sample count)."""
+    _require_gpu()
+    W, H, samps = 52, 30, 8
+    scn = ptgpu.box_mirror_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    sp = np.ascontiguousarray(scn.to_array().view(po.SPHERE_DT))
+    ca = np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT))
+    ref = _ref(scn, cam, W, H, samps)
+    with ptgpu.MultiContext(scn, cam, [0], local_shards=local) as m:
+        for br in (1, 4, 7):
+            p = ptgpu.make_params(W, H, samps, 2, SEED, br)
+            img = np.zeros((H * W, 3))
+            m.render(img, p)
+            assert np.array_equal(img, ref), br
+            m.render(img, p)
+            assert np.array_equal(img, 2.0 * ref), br
+        # a smaller frame on the same context (same scene: the camera's aspect
+        # is the scene's, the image size is the params')
+        p2 = ptgpu.make_params(W // 2, H // 2, samps, 2, SEED, 1)
+        img2 = np.zeros((H // 2 * (W // 2), 3))
+        m.render(img2, p2)
+        b, _ = po.render_xs_f32(sp, ca, W // 2, H // 2, samps, 2, SEED)
+        assert np.array_equal(img2.reshape(H // 2, W // 2, 3), b.astype(np.float64))
+        p = ptgpu.make_params(W, H, samps, 2, SEED, 2)
+        m.reset_accumulation(p)
+        done = 0
+        prev = np.zeros((H, W, 3), dtype=np.float32)
+        for end in (3, 5, samps):
+            m.accumulate(p, done, end)
+            done = end
+            m.resolve(prev, p, done)
+            b, _ = po.render_xs_f32(sp, ca, W, H, done, 2, SEED)
+            assert np.array_equal(prev, b), done
+        assert np.array_equal(prev.astype(np.float64).reshape(H * W, 3), ref)
+
+
+def test_multi_context_refuses_reference_f64_and_restores_the_device():
+    _require_gpu()
+    W, H = 16, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    torch.cuda.set_device(0)
+    with ptgpu.MultiContext(scn, cam, [0]) as m:
+        with pytest.raises(ptgpu.PtgError, match="fp32 kernel only"):
+            m.render(np.zeros((H * W, 3)), ptgpu.make_params(W, H, 2, 2, SEED, flags=ptgpu.FLAG_REFERENCE_F64))
+        with pytest.raises(ptgpu.PtgError, match="shard_count must be 1"):
+            m.render(np.zeros((H * W, 3)), ptgpu.make_params(W, H, 2, 2, SEED, 1, 0, 2))
+    with pytest.raises(ptgpu.PtgError, match="fp32 kernel only"):
+        _multi_f64(scn, cam, W, H)  # ptg_render_multi with PTG_FLAG_REFERENCE_F64
+    assert torch.cuda.current_device() == 0
+
+
+def _multi_f64(scn, cam, W, H):
+    import ctypes as C
+    sp = scn.to_array()
+    ca = cam.to_array()
+    p = ptgpu.make_params(W, H, 2, 2, SEED, flags=ptgpu.FLAG_REFERENCE_F64)
+    devs = (C.c_int * 1)(0)
+    img = np.zeros((H * W, 3))
+    from ptgpu._abi import check, lib
+    check(lib().ptg_render_multi(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), C.byref(p),
+                                 devs, 1, img.ctypes.data_as(C.c_void_p)), "ptg_render_multi")
+
+
+def test_partial_pixel_group_with_the_largest_chunk():
+    """a unit of fewer than 64 slots indexes its paths through a
+    float-reciprocal divmod that is exact for it < 2^22; fill_launch caps
+    every chunk at 2^16 samples so that 64 * chunk <= 2^22.  A 7-pixel row at
+    3x3 sub-pixels (63 slots) with 100,000 samples per sub-pixel and an
+    explicit chunk of 2^20 (capped): bit-exact with the oracle."""
+    _require_gpu()
+    W, H, samps, nsub = 7, 1, 100_000, 3
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    sp = np.ascontiguousarray(scn.to_array().view(po.SPHERE_DT))
+    ca = np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT))
+    out = torch.full((W * H * 3,), -7.0, dtype=torch.float32, device="cuda")
+    with ptgpu.Context(scn, cam) as ctx:
+        ctx.render_device(out, ptgpu.make_params(W, H, samps, nsub, SEED, chunk_samples=1 << 20))
+        torch.cuda.synchronize()
+    gpu = out.cpu().numpy().reshape(H, W, 3)
+    b, _ = po.render_xs_rect(sp, ca, W, H, samps, nsub, SEED, nthreads=16)
+    assert np.array_equal(gpu, b)

@@ -95,3 +95,24 @@ def test_mode_b_division_and_sqrt_accuracy():
     assert (r[~pos] == 0).all()
     z, rz = po.mode_b_math(np.array([0.0, -0.0, 4.0], np.float32), np.ones(3, np.float32))
     assert rz[0] == 0 and rz[1] == 0 and rz[2] == 2.0
+
+
+@pytest.mark.parametrize("name,W,H,samps,rows,cols", [("box", 64, 48, 4, (3, 40, 7), (5, 50)),
+                                                      ("synthetic:300", 64, 36, 2, (0, 36, 5), (0, 64))])
+def test_rect_renders_equal_row_renders(name, W, H, samps, rows, cols):
+    """po_render_xs_*_rect (parallel over pixels, for single rows at the
+    BASELINE sample counts) gives the row renders' bits on its rectangle and
+    leaves the rest untouched, in both arithmetic modes."""
+    import ptgpu
+    scn = ptgpu.make_scene(name, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    sp = np.ascontiguousarray(scn.to_array().view(po.SPHERE_DT))
+    ca = np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT))
+    ys = H - 1 - np.arange(*rows)
+    for f64 in (False, True):
+        r, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, 0x5EED0001, cols=cols, rows=rows, f64=f64)
+        full, _ = (po.render_xs_f64 if f64 else po.render_xs_f32)(sp, ca, W, H, samps, 2, 0x5EED0001, rows=rows)
+        assert np.array_equal(r[ys][:, cols[0]:cols[1]], full[ys][:, cols[0]:cols[1]])
+        mask = np.ones((H, W), bool)
+        mask[np.ix_(ys, np.arange(*cols))] = False
+        assert (r[mask] == 0).all() and r[~mask].sum() > 0
