@@ -266,7 +266,7 @@ def main():
     # N > 1: the same frame rendered by rank 0 alone (shard_count 1), untimed
     # with respect to `value` -- the driver's 1-GPU BENCH line is the 1080p
     # frame, so the N-GPU line carries its own same-frame T1 and efficiency
-    t1 = None
+    t1_frame = None
     if world > 1 and args.t1 == "auto":
         if rank == 0:
             p1 = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, 0, 1, args.chunk, flags=f64)
@@ -279,7 +279,7 @@ def main():
             ctx.render_device(full, p1, None, stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            t1 = {"ms": round(e0.elapsed_time(e1), 3), "wall_ms": round((time.perf_counter() - w0) * 1e3, 3)}
+            t1_frame = {"ms": round(e0.elapsed_time(e1), 3), "wall_ms": round((time.perf_counter() - w0) * 1e3, 3)}
             del full
         dist.barrier()
 
@@ -382,11 +382,12 @@ def main():
         }
         if per_rank is not None:
             out["per_rank"] = per_rank
-        if t1 is not None:
+        if t1_frame is not None:
             # efficiency of this run = T1 / (N * T_N), both on this node in this run
-            out["t1_ms"] = t1["ms"]
-            out["t1"] = dict(t1, note="the same frame on rank 0's GPU alone (HIP events; no gather), untimed for value")
-            out["efficiency"] = round(t1["ms"] / (world * elapsed / args.steps * 1e3), 4)
+            out["t1_ms"] = t1_frame["ms"]
+            out["t1"] = dict(t1_frame, note="the same frame on rank 0's GPU alone (HIP events; no gather), "
+                                            "untimed for value")
+            out["efficiency"] = round(t1_frame["ms"] / (world * elapsed / args.steps * 1e3), 4)
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)
