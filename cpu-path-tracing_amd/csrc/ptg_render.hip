@@ -152,6 +152,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_TAIL_CHUNK
 #define PTG_BVH_TAIL_CHUNK 0  // ... in chunks of this many samples (0: the auto chunk, 20 at C5 8-way; 10: +0.8 %, 32: +5 %)
 #endif
+#ifndef PTG_BVH_TAIL_PSPLIT
+#define PTG_BVH_TAIL_PSPLIT 1  // BVH kernel's split tail: units of interleaved pixels with all samples (0: sample chunks accumulated in HBM)
+#endif
 #ifndef PTG_DG_SKIP
 #define PTG_DG_SKIP 1  // shade: skip the diffuse/dielectric block when no lane of the wave needs it
 #endif
@@ -289,6 +292,13 @@ struct KArgs {
     // resolves -- no HBM accumulator (lvl_unit[l] is a multiple of the
     // waves per workgroup)
     int lvl_coop[kMaxLevels];
+    // pixel-split level (the BVH kernel's split tail): each pixel group in
+    // lvl_psplit[l] units, unit k taking the group's pixels k, k + ps, k + 2ps,
+    // ... (interleaved, so the units of a group cost about the same) with
+    // every sample (lvl_inwave: resolved in the wave, nothing accumulated in
+    // HBM); 1 elsewhere
+    int lvl_psplit[kMaxLevels];
+    int lvl_inwave[kMaxLevels];  // the level's units hold every sample of their pixels
     int needs_resolve;  // some level accumulates in HBM: resolve_kernel from resolve_row0
     long long lvl_unit[kMaxLevels + 1];
     int resolve_row0;
@@ -1291,20 +1301,26 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     const long long t = unit - A.lvl_unit[lv];
     const int nlg = A.lvl_group[lv + 1] - A.lvl_group[lv];
     const bool coop = A.lvl_coop[lv] != 0;  // wave wv of the workgroup takes chunk wv of one pixel group
-    const int group = A.lvl_group[lv] + (int)(coop ? t / kWaves : t % nlg);
+    const int ps = A.lvl_psplit[lv];        // units per pixel group (pixel-split level) or 1
+    const long long nlu = (long long)nlg * ps;  // units per sample chunk
+    const long long tg = coop ? t / kWaves : t % nlu;
+    const int group = A.lvl_group[lv] + (int)(tg / ps);
+    const int part = (int)(tg - (tg / ps) * ps);
     const int len = A.lvl_chunk[lv];
-    const int s0 = A.sample_begin + (int)(coop ? t % kWaves : t / nlg) * len;
+    const int s0 = A.sample_begin + (int)(coop ? t % kWaves : t / nlu) * len;
     if (s0 >= A.sample_end)
         return;  // whole wave: alignment padding before a cooperative level
     // the unit holds every sample of its pixels: resolve in the wave
-    const bool in_wave = lv == 0 && A.single_chunk;
+    const bool in_wave = A.lvl_inwave[lv] != 0;
     const int slab_row = group / A.waves_per_row;
     const int xblk = group - slab_row * A.waves_per_row;
     const int r = out_row_of(A, slab_row);
     const int y = A.H - 1 - r;  // main.cpp:181: y = 0 is the bottom row
-    const int x0 = xblk * A.pixels_per_wave;
-    int npix = A.W - x0;
-    npix = npix < A.pixels_per_wave ? npix : A.pixels_per_wave;
+    // the unit's pixels: x0, x0 + ps, ... (ps = 1: a contiguous group)
+    const int x0 = xblk * A.pixels_per_wave + part;
+    int npix = (A.pixels_per_wave - part + ps - 1) / ps;
+    const int left = A.W - x0 > 0 ? (A.W - x0 + ps - 1) / ps : 0;
+    npix = npix < left ? npix : left;
     const int nv = r < A.H ? npix * A.lanes_per_pixel : 0;  // valid slots are a prefix
     int cnt = A.sample_end - s0;
     cnt = cnt < len ? cnt : len;
@@ -1314,7 +1330,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     lds_acc[wv][lane + 64] = 0ull;
     lds_acc[wv][lane + 128] = 0ull;
     if (lane < nv) {
-        int px = x0 + lane / A.lanes_per_pixel;
+        int px = x0 + (lane / A.lanes_per_pixel) * ps;
         int sub = lane % A.lanes_per_pixel;
         int sy = sub / A.nsub;
         int sx = sub - sy * A.nsub;
@@ -1725,7 +1741,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 pix = mk3(__builtin_fmaf(m[0], A.inv_sub2, pix.x), __builtin_fmaf(m[1], A.inv_sub2, pix.y),
                           __builtin_fmaf(m[2], A.inv_sub2, pix.z));
             }
-            float *out = A.out + ((size_t)slab_row * A.W + x0 + lane) * 3;
+            float *out = A.out + ((size_t)slab_row * A.W + x0 + lane * ps) * 3;
             out[0] = pix.x;
             out[1] = pix.y;
             out[2] = pix.z;
@@ -2236,8 +2252,12 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.lvl_chunk[0] = chunk;
     A.lvl_unit[0] = 0;
     A.lvl_unit[1] = A.n_units;
-    for (int l = 0; l < kMaxLevels; ++l)
+    for (int l = 0; l < kMaxLevels; ++l) {
         A.lvl_coop[l] = 0;
+        A.lvl_psplit[l] = 1;
+        A.lvl_inwave[l] = 0;
+    }
+    A.lvl_inwave[0] = A.single_chunk;
     A.resolve_row0 = 0;
     A.needs_resolve = !A.single_chunk;
     // Split tail: with whole-pixel units, the grid ends when its slowest last
@@ -2267,14 +2287,22 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
             // one chunk per wave of a (linear-kernel) workgroup: the level's
             // sums stay in LDS; its first unit starts a workgroup
             const bool coop = PTG_COOP_TAIL && ctx->n <= kLinearMax && nch == kLinWaves;
+            // BVH kernel (one wave per workgroup, no cooperative level): the
+            // pixel group split into as many units of interleaved pixels,
+            // each with every sample -- the unit length of nch sample chunks,
+            // resolved in the wave (C5: no HBM atomics, no resolve pass)
+            const bool psplit = !coop && ctx->n > kLinearMax && PTG_BVH_TAIL_PSPLIT && l == 1 && nch > 1 &&
+                                A.pixels_per_wave >= nch;
             if (coop)
                 A.lvl_unit[l] = (A.lvl_unit[l] + kLinWaves - 1) / kLinWaves * kLinWaves;
-            else if (A.resolve_row0 == A.slab_rows)
+            else if (!psplit && A.resolve_row0 == A.slab_rows)
                 A.resolve_row0 = row;
             A.lvl_coop[l] = coop ? 1 : 0;
+            A.lvl_psplit[l] = psplit ? nch : 1;
+            A.lvl_inwave[l] = psplit ? 1 : 0;
             row += rows;
             rows_left -= rows;
-            A.lvl_chunk[l] = ch;
+            A.lvl_chunk[l] = psplit ? nsamp : ch;
             A.lvl_group[l + 1] = row * A.waves_per_row;
             A.lvl_unit[l + 1] = A.lvl_unit[l] + (long long)(A.lvl_group[l + 1] - A.lvl_group[l]) * nch;
         }

@@ -569,3 +569,24 @@ def test_c5_frame_size_rows_are_exact():
     for y in (0, 300):  # y = 0: the last slab row (split tail); 300: a head row in the sphere field
         ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1), nthreads=16)
         _check_equal(full[H - 1 - y], ref[H - 1 - y])
+
+
+@pytest.mark.parametrize("samps", [8, 37])
+def test_bvh_pixel_split_tail_is_exact(samps):
+    """The BVH kernel's split tail (fill_launch, PTG_BVH_TAIL_PSPLIT): the
+    last ~round of rows runs each 16-pixel group as 4 (8 for 8-way splits)
+    units of interleaved pixels with every sample (resolved in the wave, no
+    HBM accumulation) -- the frame
+    equals the same frame in explicit sample chunks, and oracle rows of the
+    tail (y = 0, 1) and the head equal the oracle's linear scan."""
+    _require_gpu()
+    W, H = 1920, 1080
+    scn = ptgpu.make_scene("synthetic:300", W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    tail, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1)
+    chunked, _ = _gpu_image(scn, cam, W, H, samps, band_rows=1, chunk=3)
+    assert np.array_equal(tail, chunked)
+    sp, ca = _oracle_scene(scn, cam)
+    for y in (0, 1, 700):
+        ref, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1), nthreads=16)
+        _check_equal(tail[H - 1 - y], ref[H - 1 - y])
