@@ -480,7 +480,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         for (; i < A.end_ax[k]; ++i)
             test(i, kind_tag);
     };
-    if (A.box_mode) {
+#ifndef PTG_ASSUME_BOX_MODE
+#define PTG_ASSUME_BOX_MODE 0  // analysis builds only (tools/isa_breakdown.py): box mode on, the other scan compiled out
+#endif
+    if (PTG_ASSUME_BOX_MODE || A.box_mode) {
         // Box mode (DESIGN.md "box mode"): per axis the wall the ray moves
         // toward and the distance u/v to its tangent plane; the wall of the
         // nearest plane is tested first.  Every wall lies beyond its tangent
@@ -1154,6 +1157,9 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #endif
     {
         PTG_STAT(4);
+#if PTG_BLOCK_STATS == 3  // debug: wave cycles of the diffuse/dielectric block in [14]
+        const unsigned long long dg_t0 = clock64();
+#endif
         float cp = 0.0f, sp = 0.0f, ra = 0.0f;
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
             const uint32_t m_phi = draw_bits(st);
@@ -1196,6 +1202,13 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
             nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
                      __builtin_fmaf(nn.z, -s3, perp.z));
         }
+#if PTG_BLOCK_STATS == 3
+        {
+            const unsigned long long dg_t1 = clock64();
+            if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)
+                atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + 14], dg_t1 - dg_t0);
+        }
+#endif
     }
     if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
         PTG_STAT(5);
@@ -1303,9 +1316,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     const bool coop = A.lvl_coop[lv] != 0;  // wave wv of the workgroup takes chunk wv of one pixel group
     const int ps = A.lvl_psplit[lv];        // units per pixel group (pixel-split level) or 1
     const long long nlu = (long long)nlg * ps;  // units per sample chunk
+    // part-major like chunk-major: neighbouring units are different pixel groups
     const long long tg = coop ? t / kWaves : t % nlu;
-    const int group = A.lvl_group[lv] + (int)(tg / ps);
-    const int part = (int)(tg - (tg / ps) * ps);
+    const int group = A.lvl_group[lv] + (int)(coop ? tg : tg % nlg);
+    const int part = coop ? 0 : (int)(tg / nlg);
     const int len = A.lvl_chunk[lv];
     const int s0 = A.sample_begin + (int)(coop ? t % kWaves : t / nlu) * len;
     if (s0 >= A.sample_end)
@@ -1334,8 +1348,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         int sub = lane % A.lanes_per_pixel;
         int sy = sub / A.nsub;
         int sx = sub - sy * A.nsub;
-        uint64_t ps = ((uint64_t)y * (uint64_t)A.W + (uint64_t)px) * (uint64_t)A.lanes_per_pixel + (uint64_t)sub;
-        lds_key[wv][lane] = key_hash(A.seed, ps);
+        const uint64_t pix_sub = ((uint64_t)y * (uint64_t)A.W + (uint64_t)px) * (uint64_t)A.lanes_per_pixel + (uint64_t)sub;
+        lds_key[wv][lane] = key_hash(A.seed, pix_sub);
         lds_pix[wv][lane] = (uint32_t)px | ((uint32_t)sx << 20) | ((uint32_t)sy << 26);
     }
     __builtin_amdgcn_wave_barrier();

@@ -36,5 +36,7 @@ ptgpu.lib().ptg_debug_stats_(st)
 cyc = [st[8 + k] for k in range(6)]
 tot = sum(cyc)
 lane_segs = int(segs.item())
-print(sys.argv[2], "wave cycles per 64 lane-segments:",
+print(sys.argv[2], scene, "wave cycles per 64 lane-segments:",
       " ".join(f"{n} {64 * c / lane_segs:.0f} ({100 * c / tot:.1f} %)" for n, c in zip(NAMES, cyc)))
+if not scene.startswith("synthetic"):  # PTG_BLOCK_STATS=3: the diffuse/dielectric block inside shade
+    print(f"  of which the diffuse/dielectric block: {64 * st[14] / lane_segs:.0f} ({100 * st[14] / tot:.1f} %)")
