@@ -383,7 +383,10 @@ inline uint16_t half_ceil(double x)
 // the largest surface, in place, so the children keep the binary tree's
 // near-first order for the octant (order_bvh).  Nodes are in depth-first
 // pre-order (a node's children follow it).
-constexpr int kWide = 4;
+#ifndef PTG_WIDE_N
+#define PTG_WIDE_N 4  // children per wide node (the kernel's walk is written for 4; 8: design studies, tools/)
+#endif
+constexpr int kWide = PTG_WIDE_N;
 constexpr int32_t kWideEmpty = (int32_t)0x80000000u;
 
 struct WideGrid {

@@ -140,6 +140,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_WIDE
 #define PTG_BVH_WIDE 1  // BVH: 4-wide nodes walked with a per-lane short stack (0: binary stackless skip walk)
 #endif
+#ifndef PTG_BVH_STACK
+#define PTG_BVH_STACK 3  // wide walk: per-lane stack entries before the continuation fallback (3: C5 -0.7 % vs 2, A/B 258.3 vs 260.1 ms)
+#endif
 #ifndef PTG_BVH_TAIL_MIN_HALF_ROUNDS
 #define PTG_BVH_TAIL_MIN_HALF_ROUNDS 6  // BVH scenes: split tail from 3 rounds of wave slots on
 #endif
@@ -688,6 +691,9 @@ struct BvhTrav {
     // everything after it in depth-first order, culled by tb), so any tree
     // depth is walked correctly with three registers.
     int s0, s1;
+#if PTG_BVH_STACK >= 3
+    int s2;
+#endif
     int res;
 #endif
 };
@@ -698,7 +704,12 @@ __device__ __forceinline__ int bvh_pop(gptr<int> cont, BvhTrav &tr)
 {
     const int v = tr.s0;
     tr.s0 = tr.s1;
+#if PTG_BVH_STACK >= 3
+    tr.s1 = tr.s2;
+    tr.s2 = -1;
+#else
     tr.s1 = -1;
+#endif
     if (v != -1)
         return v;
     const int r = tr.res;  // stack dry: the resume position, then its continuation
@@ -733,6 +744,9 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.ni = A.n_nodes > 0 ? (int)(oct << A.bvh_shift) : -1;
     tr.s0 = -1;
     tr.s1 = -1;
+#if PTG_BVH_STACK >= 3
+    tr.s2 = -1;
+#endif
     tr.res = -1;
     (void)oct_mask;
 #elif PTG_BVH_OCTANTS
@@ -847,11 +861,20 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     tr.pend = leaf ? (wf & 0x7FFFFFFF) : tr.pend;
     const int pos = base + (int)__builtin_ctz(rest | 16u);
     const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
+#if PTG_BVH_STACK >= 3
+    const bool push = rest != 0u, full = tr.s2 != -1;
+    tr.res = (push & full) ? pos : tr.res;
+    const int s0 = tr.s0, s1 = tr.s1;
+    tr.s0 = push ? (full ? -1 : e) : s0;
+    tr.s1 = push ? (full ? -1 : s0) : s1;
+    tr.s2 = push ? (full ? -1 : s1) : tr.s2;
+#else
     const bool push = rest != 0u, full = tr.s1 != -1;
     tr.res = (push & full) ? pos : tr.res;
     const int s0 = tr.s0;
     tr.s0 = push ? (full ? -1 : e) : s0;
     tr.s1 = push ? (full ? -1 : s0) : tr.s1;
+#endif
     if (next == -1) {
         next = bvh_pop(cont, tr);
         if (next < kPopLater) {  // a leaf from the stack
@@ -880,7 +903,12 @@ __device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bo
     if (need & dry & (r != -1))
         nres = cont[r >> 2];
     tr.s0 = need ? tr.s1 : v;
+#if PTG_BVH_STACK >= 3
+    tr.s1 = need ? tr.s2 : tr.s1;
+    tr.s2 = need ? -1 : tr.s2;
+#else
     tr.s1 = need ? -1 : tr.s1;
+#endif
     tr.res = nres;
     return need ? (dry ? r : v) : keep;
 }

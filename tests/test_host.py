@@ -109,6 +109,36 @@ def test_abi_rejects_bad_arguments_without_gpu_work():
         ptgpu.Context(bad, cam)
 
 
+def test_multi_abi_rejects_bad_arguments_without_gpu_work():
+    """ptg_multi_* / ptg_render_multi argument checks: NULL
+    arguments, a frame it would have to shard twice and the
+    reference-arithmetic flag are refused before any device work (here: no
+    GPU at all -- create reports PTG_ERR_NO_DEVICE and leaves *out NULL)."""
+    L = ptgpu.lib()
+    scn = ptgpu.box_scene(8, 8)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    sp, ca = scn.to_array(), cam.to_array()
+    img = np.zeros((64, 3))
+    devs = (C.c_int * 2)(0, 1)
+    args = (sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p))
+    p = ptgpu.make_params(8, 8, 4, flags=ptgpu.FLAG_REFERENCE_F64)
+    assert L.ptg_render_multi(*args, C.byref(p), devs, 2, img.ctypes.data_as(C.c_void_p)) == -4  # UNSUPPORTED
+    assert b"fp32 kernel only" in L.ptg_last_error()
+    p = ptgpu.make_params(8, 8, 4, shard_rank=1, shard_count=2)
+    assert L.ptg_render_multi(*args, C.byref(p), devs, 2, img.ctypes.data_as(C.c_void_p)) == -1
+    p = ptgpu.make_params(8, 8, 4)
+    assert L.ptg_render_multi(*args, C.byref(p), devs, 0, img.ctypes.data_as(C.c_void_p)) == -1
+    assert L.ptg_multi_render(None, C.byref(p), img.ctypes.data_as(C.c_void_p)) == -1
+    assert L.ptg_multi_resolve(None, C.byref(p), 0, None) == -1
+    assert L.ptg_multi_destroy(None) == 0
+    h = C.c_void_p(1)
+    rc = L.ptg_multi_create(*args, devs, 2, C.byref(h))
+    n = C.c_int(0)
+    L.ptg_device_count(C.byref(n))
+    if n.value == 0:  # the CPU container: no device, nothing created
+        assert rc == -3 and not h.value
+
+
 def _tilted_box():
     scn = ptgpu.make_scene("box", 64, 48)
     R = 1e6

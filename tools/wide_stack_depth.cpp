@@ -88,7 +88,7 @@ static double walk_short(const ptg_sphere *s, const BvhBuild &b, const WideGrid 
         int next = -1;
         if (ni >= 0) {
             ++steps;
-            const int base = ni & ~3, s0 = ni & 3;
+            const int base = ni & ~(kWide - 1), s0 = ni & (kWide - 1);
             int hits[kWide], nh = 0;
             for (int k = s0; k < kWide; ++k)
                 if (g_float ? box_hit_f(g, w[base + k], o, d, tb)
@@ -116,7 +116,7 @@ static double walk_short(const ptg_sphere *s, const BvhBuild &b, const WideGrid 
                     st.pop_back();
                 } else if (R != -1) {
                     next = R;
-                    R = cont[(R & ~3) / kWide];
+                    R = cont[(R & ~(kWide - 1)) / kWide];
                 } else {
                     break;
                 }
