@@ -1728,6 +1728,14 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     }
     if (parked)
         flush_parked();
+    // the lane index re-formed here (v_mbcnt of an opaque all-ones mask):
+    // taken from the work-item id it was held, and spilled, through the main
+    // loop for the epilogue's uses
+    const int lane_e = [] {
+        unsigned ones = ~0u;
+        asm volatile("" : "+s"(ones));
+        return (int)__builtin_amdgcn_mbcnt_hi(ones, __builtin_amdgcn_mbcnt_lo(ones, 0u));
+    }();
     if constexpr (kCount) {
         unsigned long long ws = segs, wsph = scnt.spheres, wbox = scnt.boxes, wbad = bad;
         for (int off = 32; off > 0; off >>= 1) {
@@ -1736,11 +1744,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             wbox += __shfl_xor(wbox, off, 64);
             wbad += __shfl_xor(wbad, off, 64);
         }
-        if (lane == 0 && A.count_nonfinite && wbad)
+        if (lane_e == 0 && A.count_nonfinite && wbad)
             atomicAdd(A.segments + 3, wbad);
-        if (lane == 0 && ws)
+        if (lane_e == 0 && ws)
             atomicAdd(A.segments, ws);
-        if (lane == 0 && A.count_tests) {
+        if (lane_e == 0 && A.count_tests) {
             atomicAdd(A.segments + 1, kBvh ? wsph : ws * (unsigned long long)A.n);
             atomicAdd(A.segments + 2, wbox);
         }
@@ -1753,7 +1761,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // wave that completes the count adds every wave's sums and resolves
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         int prev = 0;
-        if (lane == 0)
+        if (lane_e == 0)
             prev = __hip_atomic_fetch_add(&lds_coop_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         prev = __shfl(prev, 0, 64);
         coop_last = prev == kWaves - 1;
@@ -1765,10 +1773,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // the unit (or the workgroup) holds every sample of its pixels:
         // resolve here (main.cpp:195-196, same arithmetic as resolve_kernel)
         // and write 12 B per pixel -- the only HBM traffic of the frame
-        if (lane < npix && r < A.H) {
+        if (lane_e < npix && r < A.H) {
             f3 pix = mk3(0.0f, 0.0f, 0.0f);
             for (int j = 0; j < A.lanes_per_pixel; ++j) {
-                const int sl = lane * A.lanes_per_pixel + j;
+                const int sl = lane_e * A.lanes_per_pixel + j;
                 float m[3];
                 for (int c = 0; c < 3; ++c) {
                     unsigned long long sum = lds_acc[wv][sl + 64 * c];
@@ -1783,15 +1791,19 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 pix = mk3(__builtin_fmaf(m[0], A.inv_sub2, pix.x), __builtin_fmaf(m[1], A.inv_sub2, pix.y),
                           __builtin_fmaf(m[2], A.inv_sub2, pix.z));
             }
-            float *out = A.out + ((size_t)slab_row * A.W + x0 + lane * ps) * 3;
+            // opaque lane: the address is formed here, not hoisted to the
+            // unit start and held (spilled) in VGPRs through the main loop
+            int ln = lane_e;
+            asm volatile("" : "+v"(ln));
+            float *out = A.out + ((size_t)slab_row * A.W + x0 + ln * ps) * 3;
             out[0] = pix.x;
             out[1] = pix.y;
             out[2] = pix.z;
         }
-    } else if (lane < nv) {
+    } else if (lane_e < nv) {
         // several units share these pixels: exact u64 adds, resolved later
         // opaque: the address is formed here, not held in VGPRs for the unit
-        int ln = lane, row = slab_row, px0 = x0;
+        int ln = lane_e, row = slab_row, px0 = x0;
         asm volatile("" : "+v"(ln), "+s"(row), "+s"(px0));
         unsigned long long *g = A.acc + (((size_t)row * A.W + px0) * A.lanes_per_pixel + ln) * 3;
         unsigned long long vx = lds_acc[wv][ln], vy = lds_acc[wv][ln + 64], vz = lds_acc[wv][ln + 128];
