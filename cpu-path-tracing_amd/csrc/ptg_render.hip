@@ -544,6 +544,18 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                              (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             PTG_STAT(3);
+#if PTG_BLOCK_STATS == 1  // [9] waves with a lane outside the room, [10] with a lane needing a wall toward; [11], [12] such lanes
+            {
+                const unsigned long long mo = __ballot(!in_room), mn = __ballot(need[0] | need[1] | need[2]);
+                if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+                    unsigned long long *st = &ptg_dbg_stats[(blockIdx.x & 255) * 16];
+                    atomicAdd(st + 9, mo ? 1ull : 0ull);
+                    atomicAdd(st + 10, mn ? 1ull : 0ull);
+                    atomicAdd(st + 11, (unsigned long long)__popcll(mo));
+                    atomicAdd(st + 12, (unsigned long long)__popcll(mn));
+                }
+            }
+#endif
             auto wall = [&](int k, bool toward) {
                 return rec_at(walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)]);
             };

@@ -32,6 +32,11 @@ for scene in ("box", "box_mirror", "simple"):
     d["lane_segments"] = lane_segs
     d["per_wave_scan"] = {n: round(st[i] / max(1, st[1]), 3) for i, n in enumerate(NAMES)}
     d["lanes_per_wave_scan"] = round(lane_segs / max(1, st[1]), 2)
+    # extra box-mode walls: per wave-level scan, waves with a lane outside the room / needing a wall toward,
+    # and such lanes per wave-level scan
+    d["extra_walls"] = {"waves_outside": round(st[9] / max(1, st[1]), 3), "waves_need": round(st[10] / max(1, st[1]), 3),
+                        "lanes_outside": round(st[11] / max(1, st[1]), 2), "lanes_need": round(st[12] / max(1, st[1]), 2)}
     res[scene] = d
-    print(scene, json.dumps(d["per_wave_scan"]), "lanes/scan", d["lanes_per_wave_scan"], flush=True)
+    print(scene, json.dumps(d["per_wave_scan"]), "lanes/scan", d["lanes_per_wave_scan"], json.dumps(d["extra_walls"]),
+          flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "block_stats.json"), "w"), indent=1)
