@@ -381,7 +381,11 @@ constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
 constexpr float kFarPlane = 1e30f;             // box mode: the room bound of an open side
 constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall skip test
 
-enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5 };
+enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6 };
+
+#ifndef PTG_BOX_WALL_LOOP
+#define PTG_BOX_WALL_LOOP 1  // box mode: extra walls one per lane per pass, with the exact cull (0: per-axis branches)
+#endif
 
 __device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
@@ -394,7 +398,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     float bn = kInf, bq = 1.0f;
     const LinRec *best = recs + A.n;
     auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
-                        const bool valid = true) {
+                        const bool valid = true, const int ks = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
         // r is wave-uniform, except for a pair's walls / box mode
         float4 g0 = r->g.g0;
@@ -413,6 +417,29 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // up to sign), the products' bits are unchanged
             hb = __builtin_fmaf(-__builtin_fabsf(g0.w), vn, ed);
             c = __builtin_fmaf(__builtin_fabsf(g1.w), un, ee);
+        } else if constexpr (kKind == kAxSel) {
+            // the same as kAxX..kAxZ for a per-lane axis ks (box mode's extra
+            // walls).  Exact cull: with hb >= 0 the only candidate root is
+            // -c / qq, qq = sq + hb >= hb, so -c < eps hb (or c >= 0) means
+            // it fails "num < eps den" below -- the common case here, a lane
+            // that just left this convex wall; the wave skips the root when
+            // every lane is culled
+            hb = __builtin_fmaf(g0.w, comp(d, ks), ed);
+            c = __builtin_fmaf(g1.w, comp(e, ks), ee);
+            const bool live = valid & !((hb >= 0.0f) & ((c >= 0.0f) | (-c < kEps * hb)));
+#if PTG_BLOCK_STATS == 1  // [13] lanes with an extra wall in a pass, [14] of them not culled, [15] passes not skipped
+            {
+                const unsigned long long mv = __ballot(valid), ml = __ballot(live);
+                if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+                    unsigned long long *st = &ptg_dbg_stats[(blockIdx.x & 255) * 16];
+                    atomicAdd(st + 13, (unsigned long long)__popcll(mv));
+                    atomicAdd(st + 14, (unsigned long long)__popcll(ml));
+                    atomicAdd(st + 15, ml ? 1ull : 0ull);
+                }
+            }
+#endif
+            if (__ballot(live) == 0ull)
+                return;
         } else if constexpr (kKind == kBig) {  // general anchored form
             hb = __builtin_fmaf(g0.w, dot3(mk3(g1.x, g1.y, g1.z), d), ed);
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
@@ -544,6 +571,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                              (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             PTG_STAT(3);
+#if PTG_BLOCK_STATS == 3  // debug: wave cycles of the extra-wall block in [15]
+            const unsigned long long xw_t0 = clock64();
+#endif
 #if PTG_BLOCK_STATS == 1  // [9] waves with a lane outside the room, [10] with a lane needing a wall toward; [11], [12] such lanes
             {
                 const unsigned long long mo = __ballot(!in_room), mn = __ballot(need[0] | need[1] | need[2]);
@@ -556,6 +586,34 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 }
             }
 #endif
+#if PTG_BOX_WALL_LOOP
+            // each lane's extra walls in the order of the scan below (toward
+            // x, y, z, then away x, y, z): one wall per lane per pass, so a
+            // wave pays one test per pass, not one per axis any lane needs
+            unsigned m = (need[0] ? 1u : 0u) | (need[1] ? 2u : 0u) | (need[2] ? 4u : 0u);
+            if (__ballot(!in_room) != 0ull) {
+                for (int k = 0; k < 3; ++k) {
+                    float pp = A.plane_plus[k], pm = A.plane_minus[k], lo = A.pair_lo[k], hi = A.pair_hi[k];
+                    asm volatile("" : "+s"(pp), "+s"(pm), "+s"(lo), "+s"(hi));
+                    const float ok = comp(o, k);
+                    const bool pos = comp(d, k) >= 0.0f;
+                    // (the wall's existence checked by value as well: a NaN
+                    // origin must not select a missing wall's record)
+                    // (mask logic, not a select: the select became two exec-mask blocks)
+                    const bool away = (pos & !(ok >= lo) & (pm > -HUGE_VALF)) | (!pos & !(ok <= hi) & (pp < HUGE_VALF));
+                    m |= away ? 8u << k : 0u;
+                }
+            }
+            while (__ballot(m != 0u) != 0ull) {
+                const int j = __builtin_ctz(m | 64u);  // 6: none left
+                m &= m - 1u;
+                const int k = j < 3 ? j : (j < 6 ? j - 3 : 0);
+                const bool toward = j < 3;
+                const int off = walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)];
+                test_rec(rec_at(off >= 0 ? off : 0), std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
+                         (j < 6) & (off >= 0), k);
+            }
+#else
             auto wall = [&](int k, bool toward) {
                 return rec_at(walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)]);
             };
@@ -583,6 +641,14 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 if (away[2])
                     test_rec(wall(2, false), std::integral_constant<int, kAxZ>{});
             }
+#endif
+#if PTG_BLOCK_STATS == 3
+            {
+                const unsigned long long xw_t1 = clock64();
+                if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)
+                    atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + 15], xw_t1 - xw_t0);
+            }
+#endif
         }
         i = A.end_ax[2];
     } else {

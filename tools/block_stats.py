@@ -35,7 +35,11 @@ for scene in ("box", "box_mirror", "simple"):
     # extra box-mode walls: per wave-level scan, waves with a lane outside the room / needing a wall toward,
     # and such lanes per wave-level scan
     d["extra_walls"] = {"waves_outside": round(st[9] / max(1, st[1]), 3), "waves_need": round(st[10] / max(1, st[1]), 3),
-                        "lanes_outside": round(st[11] / max(1, st[1]), 2), "lanes_need": round(st[12] / max(1, st[1]), 2)}
+                        "lanes_outside": round(st[11] / max(1, st[1]), 2), "lanes_need": round(st[12] / max(1, st[1]), 2),
+                        # PTG_BOX_WALL_LOOP: per wave-level scan, lanes with a wall in a pass, those not culled, passes
+                        # that computed the root
+                        "pass_lanes": round(st[13] / max(1, st[1]), 3), "live_lanes": round(st[14] / max(1, st[1]), 3),
+                        "live_passes": round(st[15] / max(1, st[1]), 3)}
     res[scene] = d
     print(scene, json.dumps(d["per_wave_scan"]), "lanes/scan", d["lanes_per_wave_scan"], json.dumps(d["extra_walls"]),
           flush=True)

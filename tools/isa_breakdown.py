@@ -28,7 +28,7 @@ def func_lines(path):
     src = open(path).read().splitlines()
     marks = {}
     pats = {"camera_ray": r"void camera_ray\(", "scene_scan": r"const LinRec \*scene_scan\(",
-            "test_rec": r"auto test_rec = ", "box_mode": r"if \(PTG_ASSUME_BOX_MODE \|\| A\.box_mode\) \{", "axis_groups": r"\} else \{\s*$",
+            "test_rec": r"auto test_rec = ", "test_end": r"auto test = \[&\]\(const int i", "box_mode": r"if \(PTG_ASSUME_BOX_MODE \|\| A\.box_mode\) \{", "axis_groups": r"\} else \{\s*$",
             "scan_small": r"for \(; i < A\.n; \+\+i\)", "shade": r"^__device__ __forceinline__ bool shade\(const ShadeRec \*hit, float t, const float2 \*trig, f3 &o, f3 &d, f3 &T, f3 &E,$",
             "dg_block": r"if \(__ballot\(isD \| isG\) != 0ull\)", "spec_block": r"if \(spec\) \{  // main.cpp:60",
             "ray_of": r"auto ray_of = ", "begin": r"auto begin = ", "flush": r"auto flush = ",
@@ -53,7 +53,7 @@ def region_of(f, line, m):
         return "other (" + f + ")"
     if m["camera_ray"] <= line < m["scene_scan"]:
         return "camera ray"
-    if m["test_rec"] <= line < m["test_rec"] + 66:
+    if m["test_rec"] <= line < m["test_end"]:
         return "sphere test (test_rec)"
     if m["box_mode"] <= line < m["scan_small"] - 5:
         return "box-mode walls"

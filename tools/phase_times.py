@@ -40,3 +40,4 @@ print(sys.argv[2], scene, "wave cycles per 64 lane-segments:",
       " ".join(f"{n} {64 * c / lane_segs:.0f} ({100 * c / tot:.1f} %)" for n, c in zip(NAMES, cyc)))
 if not scene.startswith("synthetic"):  # PTG_BLOCK_STATS=3: the diffuse/dielectric block inside shade
     print(f"  of which the diffuse/dielectric block: {64 * st[14] / lane_segs:.0f} ({100 * st[14] / tot:.1f} %)")
+    print(f"  box mode's extra-wall block (in scan): {64 * st[15] / lane_segs:.0f} ({100 * st[15] / tot:.1f} %)")
