@@ -22,7 +22,13 @@ Also reported:
                   launch stream; peak 157.3 TFLOP/s (MI355X fp32 vector).
   cpu_baseline -- the repo's own OpenMP CPU loop (oracle/, the reference
                   algorithm in double + mt19937, "port") on a bounded sample
-                  of the same workload, rank 0 at N=1 only.
+                  of the same workload, rank 0 at N=1 only; with the quality
+                  rows of the benchmarked frame against the oracle.
+
+Arithmetic: the default (product) mode takes square roots, reciprocal
+square roots, the hit division and sin/cos from the GPU's transcendental
+instructions; --exact-math renders with PTG_FLAG_EXACT_MATH (bit for bit the
+oracle's Mode B).  Both are fp32; config.arithmetic names the mode.
 """
 import argparse
 import json
@@ -108,7 +114,8 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, row_step, gpu_image=Non
     per-pixel RMSE and max |diff| of the GPU image against the identically
     seeded fp32 CPU restatement (Mode B, the checker: 0 when bit-exact), and
     the RMSE of that against the same path in double arithmetic with the same
-    counter RNG (Mode A/xs) -- the effect of computing in fp32."""
+    counter RNG (Mode A/xs) -- the effect of computing in fp32; and the GPU
+    image's own RMSE against Mode A/xs, the north star's bar (< 1e-3)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import pyoracle as po
@@ -151,6 +158,7 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, row_step, gpu_image=Non
             "rmse_vs_cpu_fp32": float(np.sqrt(((gpu - b) ** 2).mean())),
             "max_abs_vs_cpu_fp32": float(np.abs(gpu - b).max()),
             "rmse_fp32_vs_fp64_same_rng": float(np.sqrt(((b - a) ** 2).mean())),
+            "rmse_vs_cpu_fp64_same_rng": float(np.sqrt(((gpu - a) ** 2).mean())),
             "image_mean": float(gpu.mean()),
             "seconds": round(time.perf_counter() - t1, 2),
             "checker": "oracle Mode B (fp32 restatement) / Mode A-xs (double, same counter RNG)"}
@@ -193,6 +201,8 @@ def main():
                     help="CPU baseline threads (0 = the job's CPU share: OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--cpu-row-step", type=int, default=8,
                     help="CPU baseline: time every k-th row of the frame (8 = one eighth)")
+    ap.add_argument("--exact-math", action="store_true",
+                    help="PTG_FLAG_EXACT_MATH: the exact fp32 sequences (bit for bit the CPU oracle's Mode B)")
     ap.add_argument("--reference-f64", action="store_true",
                     help="PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode, not the metric)")
     ap.add_argument("--t1", choices=["auto", "off"], default="auto",
@@ -229,7 +239,7 @@ def main():
     scn = ptgpu.make_scene(args.scene, W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     ctx = ptgpu.Context(scn, cam, device=local)
-    f64 = ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0
+    f64 = (ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
     params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
                                flags=f64)
     cparams = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
@@ -257,7 +267,7 @@ def main():
     step(count=True)
     torch.cuda.synchronize()
     seg_local, sph_local, box_local = (int(v) for v in segs.cpu().tolist())
-    if f64:  # the reference's linear scan: every sphere per segment (ref64.hpp counts segments only)
+    if args.reference_f64:  # the reference's linear scan: every sphere per segment (ref64.hpp counts segments only)
         sph_local = seg_local * ctx.n_spheres
     for _ in range(max(0, args.warmup - 1)):
         step()
@@ -351,11 +361,14 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64 (reference-arithmetic mode)" if f64 else "f32",
+            "dtype": "f64 (reference-arithmetic mode)" if args.reference_f64 else "f32",
             "data": "synthetic (procedural scene from the reference's box_scene.hpp; counter-RNG seed 0x5EED0001)",
             "config": {"workload": workload, "baseline_config": wl_name, "scene": args.scene, "width": W, "height": H, "spp": spp,
                        "samples_per_subpixel": samps, "num_subpixels": nsub, "spheres": n_sph,
                        "band_rows": args.band_rows, "chunk_samples": args.chunk or "auto",
+                       "arithmetic": ("reference f64" if args.reference_f64 else
+                                      "exact (PTG_FLAG_EXACT_MATH)" if args.exact_math else
+                                      "fast (hardware v_sqrt/v_rsq/v_rcp/v_sin/v_cos)"),
                        "parallelism": (f"tile-sharded row bands x{world}" + (" (gloo rehearsal on one GPU)"
                                                                               if rehearsal else ""))
                        if world > 1 else "single GPU"},

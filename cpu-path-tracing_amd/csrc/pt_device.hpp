@@ -135,6 +135,59 @@ __device__ __forceinline__ void sincos2pi_tab(uint32_t m, const float2 *tab, flo
     s = __builtin_fmaf(cs.y, cd, cs.x * sd);
 }
 
+// Two arithmetic modes of the render kernels (template parameter kExact):
+//  * exact (PTG_FLAG_EXACT_MATH): the deterministic sequences above -- the
+//    image equals the oracle's Mode B (oracle/pt_oracle.c) bit for bit;
+//  * fast (the default): the hardware's transcendental instructions,
+//    v_sqrt_f32 / v_rsq_f32 / v_rcp_f32 / v_sin_f32 / v_cos_f32, one
+//    instruction (issue cost of two plain VALU) instead of 8-14 -- about as
+//    accurate (~1 ulp; sin/cos of 2 pi u with v_sin/v_cos taking revolutions),
+//    but not reproducible on a CPU, so the image is tied to the reference
+//    by the north star's RMSE bar instead (DESIGN.md "arithmetic modes").
+// Everything else (draw order, the scan, the BRDFs, the exact u64 sums) is
+// the same in both modes, and a frame is deterministic in either: it does
+// not depend on sharding, unit sizes or GPU count.
+template <bool kExact>
+struct Math {
+    __device__ static __forceinline__ float rsqrt(float x) { return rsqrt_d(x); }
+    __device__ static __forceinline__ float sqrt(float x) { return sqrt_gs(x); }  // x >= 0 (or rejected later)
+    __device__ static __forceinline__ float sqrt0(float x) { return sqrt_d(x); }   // 0 for x <= 0
+    __device__ static __forceinline__ float div(float n, float d) { return div_d(n, d); }
+    __device__ static __forceinline__ void sincos2pi(uint32_t m, const float2 *tab, float &c, float &s)
+    {
+        sincos2pi_tab(m, tab, c, s);
+    }
+};
+template <>
+struct Math<false> {
+    __device__ static __forceinline__ float rsqrt(float x) { return __builtin_amdgcn_rsqf(x); }
+    __device__ static __forceinline__ float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+    __device__ static __forceinline__ float sqrt0(float x)
+    {
+        return __builtin_amdgcn_sqrtf(__int_as_float(max(__float_as_int(x), 0)));
+    }
+    // n / d for d > 0: hardware reciprocal, one residual correction (~1 ulp)
+    __device__ static __forceinline__ float div(float n, float d)
+    {
+        const float r = __builtin_amdgcn_rcpf(d);
+        const float t = n * r;
+        return __builtin_fmaf(__builtin_fmaf(-d, t, n), r, t);
+    }
+    // u = m 2^-24 in [0, 1): v_cos_f32 / v_sin_f32 take revolutions
+    __device__ static __forceinline__ void sincos2pi(uint32_t m, const float2 *, float &c, float &s)
+    {
+        const float u = (float)m * 0x1p-24f;
+        c = __builtin_amdgcn_cosf(u);
+        s = __builtin_amdgcn_sinf(u);
+    }
+};
+template <bool kExact>
+__device__ __forceinline__ f3 norm3m(f3 a)
+{
+    const float inv = Math<kExact>::rsqrt(dot3(a, a));
+    return mk3(a.x * inv, a.y * inv, a.z * inv);
+}
+
 // Host: the table, {cos, sin}(2*pi*k/128) rounded to float.  Taylor series in
 // double on the first octant (fixed operation order, no libm) and exact
 // symmetries elsewhere, so the oracle's copy (oracle/pt_oracle.c:

@@ -309,6 +309,7 @@ struct KArgs {
     int keep_acc;                  // resolve without re-zeroing (progressive previews)
     int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
     int count_nonfinite;           // PTG_FLAG_COUNT_NONFINITE: segments[3] += paths quant() would clip
+    int exact_math;                // PTG_FLAG_EXACT_MATH: the kernels' exact arithmetic (pt_device.hpp Math)
     long long n_units;
     float *out;
     unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
@@ -390,6 +391,7 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 __device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
 // Returns the winner's record, or the sentinel recs + n (no hit).
+template <bool kExact>
 __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec *recs, f3 o, f3 d, float &tbest)
 {
     // the nearest root is kept as a fraction bn/bq (bq > 0); candidates are
@@ -472,7 +474,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         }
 #endif
         // disc < 0 is rejected below whatever sq is: no clamp
-        const float sq = sqrt_scan(disc);
+        const float sq = Math<kExact>::sqrt(disc);
         const bool neg = hb < 0.0f;
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
@@ -660,7 +662,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         test(i, std::integral_constant<int, kBig>{});
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
-    tbest = best != recs + A.n ? div_d(bn, bq) : kInf;
+    tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
     return best;
 }
 
@@ -681,7 +683,7 @@ struct ScanCount {
 // g0 = {P0, R}, g1 = {n0, 2R} (huge spheres); else g0 = {C, -R^2}.
 constexpr float kReject = __builtin_nanf("");  // every comparison with it is false
 
-template <bool kBig>
+template <bool kBig, bool kExact>
 __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, const f3 o, const f3 d, const float a,
                                           const float tb)
 {
@@ -713,7 +715,7 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
     }
     if (behind | beyond | (disc < 0.0f))
         return kReject;
-    const float sq = sqrt_scan(disc);  // disc >= 0 here
+    const float sq = Math<kExact>::sqrt(disc);  // disc >= 0 here
     // the near root c/q (hb < 0, q = sq - hb), else the far root q/a, or -c/qn
     // (hb >= 0, qn = hb + sq) -- as selects (scene_scan's form: sq - hb and
     // hb + sq are the IEEE add sq + |hb|; one eps test covers the three cases),
@@ -726,7 +728,10 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
     const float den = (neg & near_lt) ? a : qq;
     if (num < kEps * den)
         return kReject;
-    return num / den;
+    if constexpr (kExact)
+        return num / den;  // IEEE: the oracle's intersect_B_lex
+    else
+        return Math<false>::div(num, den);
 }
 
 // The BVH scan's winner is its scene index (-1: none).  Ties of t go to the
@@ -804,14 +809,14 @@ __device__ __forceinline__ bool bvh_done(const KArgs &A, const BvhTrav &tr)
 
 // Start a scan: the huge spheres (tested linearly, first), then the BVH in
 // the layout of the ray's direction octant.
-template <bool kCount>
+template <bool kCount, bool kExact>
 __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt, int oct_mask)
 {
     const float a = dot3(d, d);
     tr.tb = kInf;
     tr.best = -1;
     for (int k = 0; k < A.n_big; ++k)
-        update_lex(root_lex<true>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
+        update_lex(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
 #if PTG_BVH_WIDE
@@ -1021,7 +1026,7 @@ __device__ __forceinline__ void bvh_node_step(gptr<int>, gptr<u32x4> qnodes, con
 
 // Spheres [f, f + cnt) of the leaf order against one ray: compact records
 // {C, -R^2}; (tb, best) updated by the lex rule.
-template <bool kCount>
+template <bool kCount, bool kExact>
 __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 o, f3 d, float &tb, int &best,
                                              ScanCount &sc)
 {
@@ -1029,7 +1034,7 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
     if constexpr (kCount)
         sc.spheres += cnt;
     for (int j = 0; j < cnt; ++j) {
-        const float t = root_lex<false>(A.bvh_sph[f + j], float4{}, o, d, a, tb);
+        const float t = root_lex<false, kExact>(A.bvh_sph[f + j], float4{}, o, d, a, tb);
         if (t <= tb)  // the scene index is read only for a candidate that wins or ties
             update_lex(t, A.bvh_id[f + j], tb, best);
     }
@@ -1055,7 +1060,7 @@ __device__ __forceinline__ void bvh_leaf_done(gptr<int> cont, BvhTrav &tr)
 }
 
 // The parked leaf's spheres, all by this lane.
-template <bool kCount>
+template <bool kCount, bool kExact>
 __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
     const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
@@ -1065,7 +1070,7 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 #else
     const int take = nl;
 #endif
-    leaf_spheres<kCount>(A, first, take, o, d, tr.tb, tr.best, cnt);
+    leaf_spheres<kCount, kExact>(A, first, take, o, d, tr.tb, tr.best, cnt);
     if (take < nl) {
         tr.pend = (first + take) | ((nl - take) << 24);
         return;
@@ -1082,7 +1087,7 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 // nearest roots by the same lex rule -- order-independent, so the result is
 // the one-lane result bit for bit.  pair: 2 x 64 bytes of LDS (owner lane by
 // owner rank, helper lane by helper rank).
-template <bool kCount>
+template <bool kCount, bool kExact>
 __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f3 o, f3 d, bool has,
                                                unsigned long long mhas, BvhTrav &tr, ScanCount &cnt,
                                                uint8_t (*pair)[64])
@@ -1148,7 +1153,7 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
         cnt.spheres += first_lane ? (uint32_t)mx : 0u;
     }
 #endif
-    leaf_spheres<kCount && !PTG_WAVE_STATS>(A, f, c, ro3, rd3, tb, best, cnt);
+    leaf_spheres<kCount && !PTG_WAVE_STATS, kExact>(A, f, c, ro3, rd3, tb, best, cnt);
     // owners merge their helpers' nearest roots
     const float htb = bpf(partner, tb), htb2 = bpf(partner2, tb);
     const int hbest = bpi(partner, best), hbest2 = bpi(partner2, best);
@@ -1171,15 +1176,15 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
 
 // Whole scan of one ray (parity probe kernel): walk, testing each parked leaf
 // at once.
-template <bool kCount>
+template <bool kCount, bool kExact>
 __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest, ScanCount &cnt)
 {
     BvhTrav tr;
-    bvh_start<kCount>(A, o, d, tr, cnt, A.bvh_oct_mask);
+    bvh_start<kCount, kExact>(A, o, d, tr, cnt, A.bvh_oct_mask);
     const SlabRay sr = slab_ray(A, o, d);
     while (!bvh_done(A, tr)) {
         if (tr.pend >= 0)
-            bvh_leaf<kCount>(A, (gptr<int>)A.bvh_cont, o, d, tr, cnt);
+            bvh_leaf<kCount, kExact>(A, (gptr<int>)A.bvh_cont, o, d, tr, cnt);
         else
             bvh_node_step<kCount>((gptr<int>)A.bvh_cont, (gptr<u32x4>)A.bvh_qnodes, sr, tr, cnt);
     }
@@ -1192,30 +1197,32 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
 // its radiance.
 // shade(): everything after the scene scan -- sky on a miss, else hit
 // record, emission, Russian roulette, BRDF sampling of the next ray.
+template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st);
 
-template <bool kBvh, bool kCount = false>
+template <bool kBvh, bool kExact, bool kCount = false>
 __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, const float2 *trig, f3 &o, f3 &d, f3 &T,
                                         f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
 {
     float t;
     const ShadeRec *hit;
     if constexpr (kBvh) {
-        const int id = scene_scan_bvh<kCount>(A, o, d, t, cnt);
+        const int id = scene_scan_bvh<kCount, kExact>(A, o, d, t, cnt);
         hit = id >= 0 ? A.shade + id : nullptr;
     } else {
-        const LinRec *w = scene_scan(A, recs, o, d, t);
+        const LinRec *w = scene_scan<kExact>(A, recs, o, d, t);
         hit = w != recs + A.n ? &w->s : nullptr;
     }
-    return shade(hit, t, trig, o, d, T, E, depth, st);
+    return shade<kExact>(hit, t, trig, o, d, T, E, depth, st);
 }
 
+template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st)
 {
     if (!hit) {  // main.cpp:115-120: sky
-        f3 ud = norm3(d);
+        f3 ud = norm3m<kExact>(d);
         float tt = 0.5f * (ud.y + 1.0f);
         float it = 1.0f - tt;
         E = mk3(__builtin_fmaf(T.x, __builtin_fmaf(tt, 0.5f, it), E.x),
@@ -1270,17 +1277,17 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
             const uint32_t m_phi = draw_bits(st);
             ra = draw(st);
-            sincos2pi_tab(m_phi, trig, cp, sp);
+            Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
         }
         // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
         f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
         f3 v1 = isD ? uu : d;
-        const float r1 = rsqrt_d(dot3(v1, v1));
+        const float r1 = Math<kExact>::rsqrt(dot3(v1, v1));
         v1 = mk3(v1.x * r1, v1.y * r1, v1.z * r1);
         const float x0 = -dot3(v1, nn);
         const float cthG = 1.0f < x0 ? 1.0f : x0;  // main.cpp:77
         // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
-        const float s2 = sqrt_d(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
+        const float s2 = Math<kExact>::sqrt0(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
         const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
         if (isG) {
             bool reflect = ratio * s2 > 1.0f;  // cannot refract: no Fresnel draw (main.cpp:89)
@@ -1297,7 +1304,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         // op3: diffuse -> cos theta = sqrt(1 - r); dielectric -> |r_out_parallel| (main.cpp:94)
         const f3 perp = mk3(__builtin_fmaf(nn.x, cthG, v1.x) * ratio, __builtin_fmaf(nn.y, cthG, v1.y) * ratio,
                             __builtin_fmaf(nn.z, cthG, v1.z) * ratio);
-        const float s3 = sqrt_gs(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));  // both >= 0
+        const float s3 = Math<kExact>::sqrt(isD ? 1.0f - ra : __builtin_fabsf(1.0f - dot3(perp, perp)));  // both >= 0
         if (isD) {  // main.cpp:53-55 (unit by construction, not re-normalised)
             f3 vv = cross3(nn, v1);
             float cs = cp * s2, ss = sp * s2;
@@ -1363,7 +1370,7 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // so all lanes stay busy until the pool is empty.  Path radiance is
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
-template <bool kCount, bool kBvh>
+template <bool kCount, bool kBvh, bool kExact>
 __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
     constexpr int kWaves = kBlockOf<kBvh> / 64;
@@ -1384,10 +1391,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     const float2 *trig = A.trig;
     if constexpr (kLdsGeo) {
 #if PTG_TRIG_LDS
-        __shared__ float2 lds_trig[kTrigEntries];
-        for (int i = threadIdx.x; i < kTrigEntries; i += kBlock)
-            lds_trig[i] = A.trig[i];
-        trig = lds_trig;
+        if constexpr (kExact) {  // (the fast mode's v_sin/v_cos need no table)
+            __shared__ float2 lds_trig[kTrigEntries];
+            for (int i = threadIdx.x; i < kTrigEntries; i += kBlock)
+                lds_trig[i] = A.trig[i];
+            trig = lds_trig;
+        }
 #endif
         for (int i = threadIdx.x; i <= A.n + 1; i += kBlock)  // n records + the sentinel + the wall table
             lds_lin[i] = A.lin[i];
@@ -1663,10 +1672,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if (item >= 0) {
                 if constexpr (kCount)
                     segs += 1;
-                w3 = scene_scan(A, recs, o, d, t3);
+                w3 = scene_scan<kExact>(A, recs, o, d, t3);
             }
             lin_phase(0);
-            if (item >= 0 && shade(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st))
+            if (item >= 0 && shade<kExact>(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st))
                 path_done();
             lin_phase(3);
             refill();
@@ -1676,7 +1685,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
-                if (segment<kBvh, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
+                if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
                     path_done();
             }
             refill();
@@ -1722,7 +1731,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if (item >= 0 && phase == 0) {
                 if constexpr (kCount)
                     segs += 1;
-                bvh_start<kCount && !PTG_WAVE_STATS>(A, o, d, tr, scnt, oct_mask);
+                bvh_start<kCount && !PTG_WAVE_STATS, kExact>(A, o, d, tr, scnt, oct_mask);
                 phase = bvh_done(A, tr) ? 2 : 1;
             }
             PTG_PHASE(0);
@@ -1771,11 +1780,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     // slower; pairing idle lanes with the long leaves 1.2-1.5 % faster)
                     const bool trv = phase == 1;
 #if PTG_LEAF_SPLIT
-                    bvh_leaf_split<kCount && !PTG_WAVE_STATS>(A, cont, o, d, trv && tr.pend >= 0, mhas, tr, scnt,
+                    bvh_leaf_split<kCount && !PTG_WAVE_STATS, kExact>(A, cont, o, d, trv && tr.pend >= 0, mhas, tr, scnt,
                                                                lds_pair[wv]);
 #else
                     if (trv && tr.pend >= 0)
-                        bvh_leaf<kCount && !PTG_WAVE_STATS>(A, cont, o, d, tr, scnt);
+                        bvh_leaf<kCount && !PTG_WAVE_STATS, kExact>(A, cont, o, d, tr, scnt);
 #endif
                     PTG_PHASE(2);
                     phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
@@ -1791,7 +1800,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             PTG_PHASE(5);
             if (item >= 0 && phase == 2) {
                 phase = 0;
-                if (shade(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, trig, o, d, T, E, depth, st))
+                if (shade<kExact>(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
             PTG_PHASE(3);
@@ -1922,7 +1931,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(KArgs A)
 }
 
 // Parity probe: one path per record {x, y, sx, sy, sample}.
-template <bool kBvh>
+template <bool kBvh, bool kExact>
 __global__ __launch_bounds__(kTraceBlock) void trace_kernel(KArgs A, const int32_t *coords, int n, float *out,
                                                          int32_t *segs_out)
 {
@@ -1947,12 +1956,34 @@ __global__ __launch_bounds__(kTraceBlock) void trace_kernel(KArgs A, const int32
     while (!done) {
         segs += 1;
         ScanCount scnt;
-        done = segment<kBvh>(A, A.lin, A.trig, o, d, T, E, depth, st, scnt);
+        done = segment<kBvh, kExact>(A, A.lin, A.trig, o, d, T, E, depth, st, scnt);
     }
     out[3 * i + 0] = E.x;
     out[3 * i + 1] = E.y;
     out[3 * i + 2] = E.z;
     segs_out[i] = segs;
+}
+
+// ptg_math_probe_device: the primitives as the render kernels call them
+template <bool kExact>
+__global__ __launch_bounds__(256) void math_probe_kernel(int op, const float *in, float *out, int n,
+                                                         const float2 *trig)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    if (op == PTG_PROBE_SQRT) {
+        out[i] = Math<kExact>::sqrt(in[i]);
+    } else if (op == PTG_PROBE_RSQRT) {
+        out[i] = Math<kExact>::rsqrt(in[i]);
+    } else if (op == PTG_PROBE_DIV) {
+        out[i] = Math<kExact>::div(in[2 * i], in[2 * i + 1]);
+    } else {
+        float c, s;
+        Math<kExact>::sincos2pi(__float_as_uint(in[i]) & 0xFFFFFFu, trig, c, s);
+        out[2 * i] = c;
+        out[2 * i + 1] = s;
+    }
 }
 
 __global__ void unshard_kernel(const float *__restrict__ src, float *__restrict__ dst, int W, int band_rows,
@@ -2340,6 +2371,7 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.keep_acc = 0;
     A.count_tests = (p->flags & PTG_FLAG_COUNT_TESTS) != 0;
     A.count_nonfinite = (p->flags & PTG_FLAG_COUNT_NONFINITE) != 0;
+    A.exact_math = (p->flags & PTG_FLAG_EXACT_MATH) != 0;
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
@@ -2819,12 +2851,18 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
         return PTG_OK;
     const bool bvh = A.n > kLinearMax;
     const size_t lds = bvh ? 0 : (size_t)(A.n + 2) * sizeof(LinRec);
-    if (count)
-        bvh ? render_kernel<true, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A)
-            : render_kernel<true, false><<<grid, kBlock, lds, s>>>(A);
-    else
-        bvh ? render_kernel<false, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A)
-            : render_kernel<false, false><<<grid, kBlock, lds, s>>>(A);
+    // the exact mode's sin/cos table has its own LDS (render_kernel)
+    const int sel = (count ? 4 : 0) | (bvh ? 2 : 0) | (A.exact_math ? 1 : 0);
+    switch (sel) {
+    case 0: render_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A); break;
+    case 1: render_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A); break;
+    case 2: render_kernel<false, true, false><<<grid, PTG_BVH_BLOCK, 0, s>>>(A); break;
+    case 3: render_kernel<false, true, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A); break;
+    case 4: render_kernel<true, false, false><<<grid, kBlock, lds, s>>>(A); break;
+    case 5: render_kernel<true, false, true><<<grid, kBlock, lds, s>>>(A); break;
+    case 6: render_kernel<true, true, false><<<grid, PTG_BVH_BLOCK, 0, s>>>(A); break;
+    default: render_kernel<true, true, true><<<grid, PTG_BVH_BLOCK, 0, s>>>(A); break;
+    }
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }
@@ -3000,10 +3038,35 @@ int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const i
         return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int blocks = (int)((n + kTraceBlock - 1) / kTraceBlock);
-    if (A.n > kLinearMax)
-        trace_kernel<true><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+    const bool bvh = A.n > kLinearMax;
+    if (A.exact_math)
+        bvh ? trace_kernel<true, true><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs)
+            : trace_kernel<false, true><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
     else
-        trace_kernel<false><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+        bvh ? trace_kernel<true, false><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs)
+            : trace_kernel<false, false><<<blocks, kTraceBlock, 0, s>>>(A, d_coords, (int)n, d_out, d_segs);
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int ptg_math_probe_device(ptg_context *ctx, int32_t op, int32_t exact, const float *d_in, float *d_out, size_t n,
+                          void *stream)
+{
+    if (!ctx || (n && (!d_in || !d_out)))
+        return fail(PTG_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (op < PTG_PROBE_SQRT || op > PTG_PROBE_SINCOS)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "unknown probe op");
+    if (n > (size_t)INT32_MAX / 2)
+        return fail(PTG_ERR_UNSUPPORTED, "too many operands");
+    if (n == 0)
+        return PTG_OK;
+    PTG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (exact)
+        math_probe_kernel<true><<<blocks, 256, 0, s>>>(op, d_in, d_out, (int)n, ctx->d_trig);
+    else
+        math_probe_kernel<false><<<blocks, 256, 0, s>>>(op, d_in, d_out, (int)n, ctx->d_trig);
     PTG_HIP(hipGetLastError());
     return PTG_OK;
 }

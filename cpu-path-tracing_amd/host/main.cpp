@@ -5,7 +5,7 @@
 //   pt_render_gpu [spp] [scene] [width height] [out.ppm]        (positional, as before)
 //   pt_render_gpu [--spp N] [--scene NAME|FILE] [--width W] [--height H] [--seed S]
 //                 [--devices 0,1,...] [--out FILE] [--format p3|p6]
-//                 [--save-scene FILE] [--dump-json FILE] [--no-render]
+//                 [--save-scene FILE] [--dump-json FILE] [--no-render] [--exact-math]
 //
 //   spp      total samples per pixel (main.cpp:206: divided by the 4 sub-pixels), default 4
 //   scene    box_mirror (the reference binary's scene, main.cpp:25,208) | box | simple |
@@ -16,6 +16,8 @@
 //            device list (default: the current device, ptg_render)
 //   out      P3 (the reference's format) or P6 PPM, gamma-1/2.2 8-bit values
 //            (main.cpp:240-247, utils.cpp:11-16)
+//   --exact-math  the kernel's exact arithmetic (PTG_FLAG_EXACT_MATH): the image equals
+//            the CPU oracle's bit for bit (default: the GPU's fast transcendentals)
 //   --save-scene / --dump-json write the scene (scene file) / the scene and the
 //            camera::with_config result (JSON, 17 digits) and need no GPU with --no-render
 #include <chrono>
@@ -105,6 +107,7 @@ int main(int argc, char *argv[])
     std::string scene_name = "box_mirror", out = "image.ppm", format = "p3", save_scene, dump, devices = "-1";
     std::uint64_t seed = pt::gpu::default_seed;
     bool render = true;
+    int flags = 0;
     if (argc > 1 && std::strncmp(argv[1], "--", 2) != 0) {  // the positional form
         spp = std::atoi(argv[1]);
         if (argc > 2)
@@ -147,6 +150,8 @@ int main(int argc, char *argv[])
                 dump = val();
             else if (a == "--no-render")
                 render = false;
+            else if (a == "--exact-math")
+                flags |= PTG_FLAG_EXACT_MATH;
             else {
                 std::fprintf(stderr, "unknown option %s\n", a.c_str());
                 return 2;
@@ -181,7 +186,7 @@ int main(int argc, char *argv[])
     auto const t0 = std::chrono::steady_clock::now();
     int rc = PTG_OK;
     if (nd == 1 && devs[0] < 0) {  // main.cpp:214-236 replaced by one call
-        rc = pt::gpu::render_image(some_scene, cam, image, width, height, samps, num_subpixels, seed);
+        rc = pt::gpu::render_image(some_scene, cam, image, width, height, samps, num_subpixels, seed, -1, flags);
     } else {  // several GPUs of this process: shards + one RCCL gather
         ptg_params p{};
         p.width = width;
@@ -192,6 +197,7 @@ int main(int argc, char *argv[])
         p.band_rows = 1;
         p.shard_rank = 0;
         p.shard_count = 1;
+        p.flags = flags;
         rc = ptg_render_multi(reinterpret_cast<ptg_sphere const *>(some_scene.spheres.data()), some_scene.spheres.size(),
                               reinterpret_cast<ptg_camera const *>(&cam), &p, devs.data(), nd,
                               reinterpret_cast<double *>(image.data()));

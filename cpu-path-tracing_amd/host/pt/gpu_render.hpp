@@ -40,7 +40,8 @@ inline constexpr std::uint64_t default_seed = 0x5EED0001ull;
 
 // main.cpp:214-236 replacement.  `samps` is per sub-pixel (main.cpp:206).
 inline int render_image(scene const &scn, camera const &cam, std::vector<vec3> &image, int width, int height,
-                        int samps, int num_subpixels = 2, std::uint64_t seed = default_seed, int device = -1)
+                        int samps, int num_subpixels = 2, std::uint64_t seed = default_seed, int device = -1,
+                        int flags = 0)
 {
     if (image.size() != static_cast<std::size_t>(width) * static_cast<std::size_t>(height))
         return PTG_ERR_INVALID_ARGUMENT;
@@ -53,6 +54,7 @@ inline int render_image(scene const &scn, camera const &cam, std::vector<vec3> &
     p.band_rows = 1;  // single-row bands: equal shards whenever shard_count divides H
     p.shard_rank = 0;
     p.shard_count = 1;
+    p.flags = flags;  // e.g. PTG_FLAG_EXACT_MATH: bit for bit the CPU oracle's image
     return ptg_render(reinterpret_cast<ptg_sphere const *>(scn.spheres.data()), scn.spheres.size(),
                       reinterpret_cast<ptg_camera const *>(&cam), &p, device,
                       reinterpret_cast<double *>(image.data()));

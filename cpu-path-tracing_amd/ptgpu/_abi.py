@@ -20,7 +20,7 @@ EXPORTS = (
     "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
     "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device", "ptg_scene_layout",
     "ptg_render_multi", "ptg_multi_create", "ptg_multi_destroy", "ptg_multi_render",
-    "ptg_multi_reset_accumulation", "ptg_multi_accumulate", "ptg_multi_resolve",
+    "ptg_multi_reset_accumulation", "ptg_multi_accumulate", "ptg_multi_resolve", "ptg_math_probe_device",
 )
 
 
@@ -61,6 +61,7 @@ def lib():
             "ptg_unshard_device": (I, [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P]),
             "ptg_tonemap_device": (I, [P, P, C.c_size_t, P]),
             "ptg_trace_samples_device": (I, [P, C.POINTER(Params), P, C.c_size_t, P, P, P]),
+            "ptg_math_probe_device": (I, [P, C.c_int32, C.c_int32, P, P, C.c_size_t, P]),
             "ptg_reset_accumulation_device": (I, [P, C.POINTER(Params), P]),
             "ptg_accumulate_device": (I, [P, C.POINTER(Params), C.c_int32, C.c_int32, P, P]),
             "ptg_resolve_device": (I, [P, C.POINTER(Params), C.c_int32, P, P]),

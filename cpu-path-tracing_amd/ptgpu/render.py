@@ -47,6 +47,7 @@ def _camera_array(cam) -> np.ndarray:
 FLAG_COUNT_TESTS = 1  # include/ptgpu.h PTG_FLAG_COUNT_TESTS
 FLAG_COUNT_NONFINITE = 2  # include/ptgpu.h PTG_FLAG_COUNT_NONFINITE (4 counters)
 FLAG_REFERENCE_F64 = 4  # include/ptgpu.h PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode)
+FLAG_EXACT_MATH = 8  # include/ptgpu.h PTG_FLAG_EXACT_MATH: exact sequences, bit for bit the oracle's Mode B
 
 
 def _n_counters(flags: int) -> int:
@@ -103,7 +104,8 @@ def render(scn, cam, image: np.ndarray, width: int, height: int, samples: int, n
 
 
 def render_multi(scn, cam, image: np.ndarray, width: int, height: int, samples: int, devices,
-                 num_subpixels: int = 2, seed: int = DEFAULT_SEED, band_rows: int = DEFAULT_BAND_ROWS) -> np.ndarray:
+                 num_subpixels: int = 2, seed: int = DEFAULT_SEED, band_rows: int = DEFAULT_BAND_ROWS,
+                 flags: int = 0) -> np.ndarray:
     """ptg_render_multi: the drop-in render over several GPUs of this process
     (distinct devices) -- shards rendered concurrently, ONE RCCL gather to
     devices[0], un-shard there; the image equals render()'s bit for bit."""
@@ -111,7 +113,7 @@ def render_multi(scn, cam, image: np.ndarray, width: int, height: int, samples: 
     ca = _camera_array(cam)
     if image.dtype != np.float64 or not image.flags["C_CONTIGUOUS"] or image.size != width * height * 3:
         raise ValueError("image must be a C-contiguous float64 array of width*height*3 values")
-    p = make_params(width, height, samples, num_subpixels, seed, band_rows)
+    p = make_params(width, height, samples, num_subpixels, seed, band_rows, flags=flags)
     devs = (C.c_int * len(devices))(*[int(d) for d in devices])
     check(lib().ptg_render_multi(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), C.byref(p),
                                  devs, len(devices), image.ctypes.data_as(C.c_void_p)), "ptg_render_multi")
@@ -295,6 +297,32 @@ class Context:
                                              C.c_void_p(out.data_ptr()), C.c_void_p(segs.data_ptr()),
                                              C.c_void_p(s)), "ptg_trace_samples_device")
         return out, segs
+
+    PROBE_OPS = {"sqrt": 0, "rsqrt": 1, "div": 2, "sincos": 3}  # include/ptgpu.h PTG_PROBE_*
+
+    def math_probe(self, op: str, x, exact: bool):
+        """The kernels' arithmetic primitive `op` on a float32 CUDA tensor:
+        sqrt / rsqrt of x [n]; div of x [n, 2] (x[:, 0] / x[:, 1]); sincos of
+        24-bit integers m (x: int32 [n]) -> [n, 2] (cos, sin of 2 pi m 2^-24)."""
+        import torch
+        code = self.PROBE_OPS[op]
+        x = x.contiguous()
+        if op == "div":
+            if x.dim() != 2 or x.shape[1] != 2:
+                raise ValueError("div takes [n, 2] operands")
+            n = x.shape[0]
+        else:
+            n = x.numel()
+        if op == "sincos":
+            self._check(x, torch.int32, n)
+            x = x.view(torch.float32)
+        else:
+            self._check(x, torch.float32, x.numel())
+        out = torch.empty((n, 2) if op == "sincos" else (n,), dtype=torch.float32, device=x.device)
+        s = self._stream(None)
+        check(lib().ptg_math_probe_device(self._h, code, 1 if exact else 0, C.c_void_p(x.data_ptr()),
+                                          C.c_void_p(out.data_ptr()), n, C.c_void_p(s)), "ptg_math_probe_device")
+        return out
 
 
 def _check_tensor(t, dtype, min_numel):

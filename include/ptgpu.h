@@ -103,6 +103,16 @@ typedef struct ptg_params {
  * doubles; ptg_render_device rounds them into its float slab.  Not for
  * progressive passes or trace_samples (PTG_ERR_UNSUPPORTED). */
 #define PTG_FLAG_REFERENCE_F64 4
+/* PTG_FLAG_EXACT_MATH: the fp32 kernel with deterministic square root,
+ * reciprocal square root, division and sin/cos sequences (~1 ulp) that the
+ * oracle (oracle/pt_oracle.c, Mode B) executes too -- the image then equals
+ * the CPU restatement bit for bit.  Without it (the default) the kernel uses
+ * the GPU's own v_sqrt/v_rsq/v_rcp/v_sin/v_cos instructions, about as
+ * accurate but not reproducible on a CPU: the image is within the north
+ * star's per-pixel RMSE of the reference arithmetic (DESIGN.md "arithmetic
+ * modes").  Either way a frame does not depend on sharding, work-unit sizes,
+ * progressive passes or the GPU count. */
+#define PTG_FLAG_EXACT_MATH 8
 
 typedef struct ptg_context ptg_context;
 
@@ -209,6 +219,21 @@ int ptg_scene_layout(const ptg_sphere *spheres, size_t n_spheres, const ptg_came
  * one path, main.cpp:191); d_segs n int32 (scene scans of that path). */
 int ptg_trace_samples_device(ptg_context *ctx, const ptg_params *params, const int32_t *d_coords, size_t n,
                              float *d_out, int32_t *d_segs, void *stream);
+
+/* Accuracy probe of the kernels' arithmetic primitives in either mode
+ * (exact != 0: PTG_FLAG_EXACT_MATH's sequences; 0: the hardware
+ * instructions), n operands on the device: op PTG_PROBE_SQRT out[i] =
+ * sqrt(in[i]); PTG_PROBE_RSQRT 1/sqrt(in[i]); PTG_PROBE_DIV in[2i] /
+ * in[2i+1] (divisor > 0); PTG_PROBE_SINCOS the bits of in[i] are a 24-bit
+ * integer m, out[2i], out[2i+1] = cos, sin of 2 pi m 2^-24 (main.cpp:55's
+ * phi).  The arithmetic the render kernels execute, not a separate
+ * implementation (tests/test_gpu_fast_math.py). */
+#define PTG_PROBE_SQRT 0
+#define PTG_PROBE_RSQRT 1
+#define PTG_PROBE_DIV 2
+#define PTG_PROBE_SINCOS 3
+int ptg_math_probe_device(ptg_context *ctx, int32_t op, int32_t exact, const float *d_in, float *d_out, size_t n,
+                          void *stream);
 
 #ifdef __cplusplus
 }

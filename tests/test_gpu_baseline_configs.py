@@ -16,7 +16,11 @@ the sample count, so they are rendered here at the full count:
   1e-3 vs Mode A/xs.  (Round 2 checked C5 only at 64 spp, where the fp32
   floor is 1.1e-3.)
 
-The oracle renders these rows in parallel over pixels (po_render_xs_*_rect).
+Both arithmetic modes: the default one (the GPU's v_sqrt/v_rsq/v_rcp/v_sin/
+v_cos) is held to the RMSE bar and the shard equality; the exact one
+(PTG_FLAG_EXACT_MATH) in addition to Mode B bit for bit.  The oracle renders
+these rows in parallel over pixels (po_render_xs_*_rect), once per row for
+both modes.
 """
 import os
 
@@ -32,6 +36,8 @@ import pyoracle as po  # noqa: E402
 SEED = 0x5EED0001
 NORTH_STAR_RMSE = 1e-3
 NT = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
+EXACT = ptgpu.FLAG_EXACT_MATH
+MODES = [pytest.param(0, id="fast"), pytest.param(EXACT, id="exact")]
 _cache = {}
 
 
@@ -55,10 +61,10 @@ def _arrays(scn):
             np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT)))
 
 
-def _frame(name, W, H, samps, shards=1):
+def _frame(name, W, H, samps, shards=1, mode=0):
     """The frame on one GPU (shards = 1) or as `shards` interleaved single-row
     band slabs gathered rank-major and un-sharded on the device."""
-    key = (name, W, H, samps, shards)
+    key = (name, W, H, samps, shards, mode)
     if key not in _cache:
         scn = ptgpu.make_scene(name, W, H)
         cam, _, _ = _arrays(scn)
@@ -66,7 +72,7 @@ def _frame(name, W, H, samps, shards=1):
         gathered = torch.full((shards, rows * W * 3), -7.0, dtype=torch.float32, device="cuda")
         with ptgpu.Context(scn, cam) as ctx:
             for k in range(shards):
-                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, shards))
+                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, shards, flags=mode))
             image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
             ptgpu.unshard_device(gathered, image, W, H, 1, shards)
             torch.cuda.synchronize()
@@ -75,72 +81,90 @@ def _frame(name, W, H, samps, shards=1):
     return _cache[key]
 
 
-def _rows_vs_oracle(name, W, H, samps, gpu, y, cols):
+def _oracle_row(name, W, H, samps, y, cols, f64):
+    """Mode B (f64 False) or Mode A/xs (True) pixels cols of row y, cached:
+    the two arithmetic modes are checked against the same oracle rows."""
+    key = ("oracle", name, W, H, samps, y, cols, f64)
+    if key not in _cache:
+        scn = ptgpu.make_scene(name, W, H)
+        _, sp, ca = _arrays(scn)
+        img, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, cols=cols, rows=(y, y + 1, 1), nthreads=NT,
+                                   f64=f64)
+        _cache[key] = img[H - 1 - y, cols[0]:cols[1]].astype(np.float64)
+    return _cache[key]
+
+
+def _rows_vs_oracle(name, W, H, samps, gpu, y, cols, mode):
     """Row y (image space, main.cpp:181: y = 0 at the bottom), pixels cols:
-    bit-exact vs Mode B; returns the squared errors vs Mode A/xs."""
-    scn = ptgpu.make_scene(name, W, H)
-    _, sp, ca = _arrays(scn)
-    x0, x1 = cols
-    b, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, cols=cols, rows=(y, y + 1, 1), nthreads=NT)
-    g = gpu[H - 1 - y, x0:x1]
-    bb = b[H - 1 - y, x0:x1]
-    diff = np.abs(g.astype(np.float64) - bb.astype(np.float64))
-    assert float(diff.max()) == 0.0, (y, float(diff.max()), int((diff > 0).sum()))
-    a, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, cols=cols, rows=(y, y + 1, 1), nthreads=NT, f64=True)
-    return (g.astype(np.float64) - a[H - 1 - y, x0:x1]) ** 2
+    bit-exact vs Mode B in the exact mode; returns the squared errors vs Mode
+    A/xs and the RMSE vs Mode B."""
+    g = gpu[H - 1 - y, cols[0]:cols[1]].astype(np.float64)
+    b = _oracle_row(name, W, H, samps, y, cols, False)
+    diff = np.abs(g - b)
+    if mode == EXACT:
+        assert float(diff.max()) == 0.0, (y, float(diff.max()), int((diff > 0).sum()))
+    a = _oracle_row(name, W, H, samps, y, cols, True)
+    return (g - a) ** 2, float(np.sqrt((diff ** 2).mean()))
 
 
 C4 = ("box", 3840, 2160, 1024)  # BASELINE configs[3]: 4096 spp = 1024 samples per sub-pixel
 C5 = ("synthetic:10000", 1920, 1080, 256)  # configs[4]: 1024 spp
 
 
-def test_c4_full_spp_eight_shards_equal_the_frame():
+@pytest.mark.parametrize("mode", MODES)
+def test_c4_full_spp_eight_shards_equal_the_frame(mode):
     _require_gpu()
-    full = _frame(*C4)
-    sharded = _frame(*C4, shards=8)
+    full = _frame(*C4, mode=mode)
+    sharded = _frame(*C4, shards=8, mode=mode)
     assert np.array_equal(full, sharded)
     assert full.min() >= 0.0 and full.max() <= 1.0 and full.mean() > 0.02
 
 
 # y = 0, 1: the last slab rows (the split tail of the one-GPU frame and of each
 # 8-way shard); 1337, H - 1: head rows
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("y", [0, 1, 1337, 2159])
-def test_c4_full_spp_rows_vs_oracle(y):
+def test_c4_full_spp_rows_vs_oracle(y, mode):
     _require_gpu()
     name, W, H, samps = C4
-    sq = _rows_vs_oracle(name, W, H, samps, _frame(*C4), y, (0, W))
+    sq, rmse_b = _rows_vs_oracle(name, W, H, samps, _frame(*C4, mode=mode), y, (0, W), mode)
     rmse = float(np.sqrt(sq.mean()))
-    _record(config="C4", y=y, cols=[0, W], rmse_vs_mode_a_xs=rmse)
+    _record(config="C4", mode="exact" if mode else "fast", y=y, cols=[0, W], rmse_vs_mode_a_xs=rmse,
+            rmse_vs_mode_b=rmse_b)
     assert rmse < NORTH_STAR_RMSE, (y, rmse)
-    _cache.setdefault("c4_sq", []).append(sq)
+    _cache.setdefault(("c4_sq", mode), []).append(sq)
 
 
-def test_c4_full_spp_rmse_over_rows():
-    sq = _cache.get("c4_sq")
+@pytest.mark.parametrize("mode", MODES)
+def test_c4_full_spp_rmse_over_rows(mode):
+    sq = _cache.get(("c4_sq", mode))
     if not sq:
         pytest.skip("needs test_c4_full_spp_rows_vs_oracle")
     rmse = float(np.sqrt(np.concatenate([s.reshape(-1) for s in sq]).mean()))
-    _record(config="C4", rows="all", rmse_vs_mode_a_xs=rmse)
+    _record(config="C4", mode="exact" if mode else "fast", rows="all", rmse_vs_mode_a_xs=rmse)
     assert rmse < NORTH_STAR_RMSE, rmse
 
 
 # y = 300: head row across the sphere field; y = 2: a split-tail row (the BVH
 # frame's last ~69 slab rows); each row in two halves
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("y,cols", [(300, (0, 960)), (300, (960, 1920)), (2, (0, 960)), (2, (960, 1920))])
-def test_c5_full_spp_rows_vs_oracle(y, cols):
+def test_c5_full_spp_rows_vs_oracle(y, cols, mode):
     _require_gpu()
     name, W, H, samps = C5
-    sq = _rows_vs_oracle(name, W, H, samps, _frame(*C5), y, cols)
+    sq, rmse_b = _rows_vs_oracle(name, W, H, samps, _frame(*C5, mode=mode), y, cols, mode)
     rmse = float(np.sqrt(sq.mean()))
-    _record(config="C5", y=y, cols=list(cols), rmse_vs_mode_a_xs=rmse)
+    _record(config="C5", mode="exact" if mode else "fast", y=y, cols=list(cols), rmse_vs_mode_a_xs=rmse,
+            rmse_vs_mode_b=rmse_b)
     assert rmse < NORTH_STAR_RMSE, (y, cols, rmse)
-    _cache.setdefault("c5_sq", []).append(sq)
+    _cache.setdefault(("c5_sq", mode), []).append(sq)
 
 
-def test_c5_full_spp_rmse_over_rows():
-    sq = _cache.get("c5_sq")
+@pytest.mark.parametrize("mode", MODES)
+def test_c5_full_spp_rmse_over_rows(mode):
+    sq = _cache.get(("c5_sq", mode))
     if not sq:
         pytest.skip("needs test_c5_full_spp_rows_vs_oracle")
     rmse = float(np.sqrt(np.concatenate([s.reshape(-1) for s in sq]).mean()))
-    _record(config="C5", rows="all", rmse_vs_mode_a_xs=rmse)
+    _record(config="C5", mode="exact" if mode else "fast", rows="all", rmse_vs_mode_a_xs=rmse)
     assert rmse < NORTH_STAR_RMSE, rmse

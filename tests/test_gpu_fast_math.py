@@ -1,0 +1,215 @@
+"""The default arithmetic mode (DESIGN.md "arithmetic modes").
+
+Without PTG_FLAG_EXACT_MATH the kernels take square roots, reciprocal square
+roots, the nearest hit's division and the diffuse sin/cos from the GPU's own
+v_sqrt_f32 / v_rsq_f32 / v_rcp_f32 / v_sin_f32 / v_cos_f32 instead of the
+deterministic sequences the oracle's Mode B executes.  A CPU cannot
+reproduce those instructions bit for bit, so here:
+
+* the primitives' accuracy is measured against float64 on 2^20 operands each
+  (the exact mode's sequences equal the oracle's Mode B primitives bit for
+  bit on the same operands);
+* frames of every scene kind are held to the north star's per-pixel RMSE
+  against Mode A/xs (the reference's double arithmetic, same draws), no
+  worse than the exact mode's own distance to it;
+* everything that must not change a bit still does not: GPU frames equal
+  themselves across work-unit sizes, split tails, BVH unit levels, 2/4/8-way
+  shards and progressive passes (GPU against GPU, bit for bit).
+
+The C1-C5 configs at their BASELINE sizes are checked in both modes in
+test_gpu_reference.py and test_gpu_baseline_configs.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ptgpu  # noqa: E402
+import pyoracle as po  # noqa: E402
+
+SEED = 0x5EED0001
+EXACT = ptgpu.FLAG_EXACT_MATH
+NORTH_STAR_RMSE = 1e-3
+NT = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a visible MI355X")
+
+
+def _arrays(scn):
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    return (cam, np.ascontiguousarray(scn.to_array().view(po.SPHERE_DT)),
+            np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT)))
+
+
+def _image(scn, cam, W, H, samps, flags=0, band_rows=1, rank=0, count=1, chunk=0):
+    p = ptgpu.make_params(W, H, samps, 2, SEED, band_rows, rank, count, chunk, flags=flags)
+    rows = ptgpu.shard_rows(H, band_rows, count)
+    out = torch.full((rows * W * 3,), -7.0, dtype=torch.float32, device="cuda")
+    with ptgpu.Context(scn, cam) as ctx:
+        ctx.render_device(out, p)
+        torch.cuda.synchronize()
+    img = out.cpu().numpy().reshape(rows, W, 3)
+    return img[:H] if count == 1 else img
+
+
+def _ulp_err(got, ref64):
+    """|got - ref| in units of the float32 spacing at ref."""
+    ref32 = ref64.astype(np.float32)
+    ulp = np.spacing(np.abs(ref32)).astype(np.float64)
+    return np.abs(got.astype(np.float64) - ref64) / ulp
+
+
+# ---- primitives ------------------------------------------------------------
+
+N_OPS = 1 << 20
+
+
+def _operands():
+    rng = np.random.default_rng(20251017)
+    x = np.exp(rng.uniform(np.log(1e-12), np.log(1e12), N_OPS)).astype(np.float32)
+    d = np.exp(rng.uniform(np.log(1e-6), np.log(1e6), N_OPS)).astype(np.float32)
+    m = np.concatenate([rng.integers(0, 1 << 24, N_OPS - 8, dtype=np.int64),
+                        [0, 1, (1 << 22) - 1, 1 << 22, 1 << 23, (3 << 22) + 5, (1 << 24) - 2, (1 << 24) - 1]])
+    return x, d, m.astype(np.int32)
+
+
+def test_primitive_accuracy_and_exact_mode_bits():
+    """Fast primitives within a few ulp of float64 (sin/cos within an
+    absolute 2e-6 of 2 pi m 2^-24's); the exact mode's primitives equal the
+    oracle's Mode B ones bit for bit (the kernels' own arithmetic, through
+    ptg_math_probe_device).  The measured maxima are printed for DESIGN.md."""
+    _require_gpu()
+    scn = ptgpu.box_scene(8, 8)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    x, d, m = _operands()
+    xg = torch.from_numpy(x).cuda()
+    pairs = torch.from_numpy(np.stack([x, d], axis=1)).cuda()
+    mg = torch.from_numpy(m).cuda()
+    with ptgpu.Context(scn, cam) as ctx:
+        got = {(op, ex): ctx.math_probe(op, arg, ex).cpu().numpy()
+               for op, arg in (("sqrt", xg), ("rsqrt", xg), ("div", pairs), ("sincos", mg)) for ex in (False, True)}
+    x64, d64 = x.astype(np.float64), d.astype(np.float64)
+    phi = 2.0 * np.pi * m.astype(np.float64) * 2.0 ** -24
+    err = {"sqrt": _ulp_err(got["sqrt", False], np.sqrt(x64)).max(),
+           "rsqrt": _ulp_err(got["rsqrt", False], 1.0 / np.sqrt(x64)).max(),
+           "div": _ulp_err(got["div", False], x64 / d64).max(),
+           "sincos_abs": max(np.abs(got["sincos", False][:, 0] - np.cos(phi)).max(),
+                             np.abs(got["sincos", False][:, 1] - np.sin(phi)).max())}
+    err_exact = {"sqrt": _ulp_err(got["sqrt", True], np.sqrt(x64)).max(),
+                 "rsqrt": _ulp_err(got["rsqrt", True], 1.0 / np.sqrt(x64)).max(),
+                 "div": _ulp_err(got["div", True], x64 / d64).max()}
+    print("fast primitives:", {k: float(v) for k, v in err.items()}, "exact:",
+          {k: float(v) for k, v in err_exact.items()})
+    assert err["sqrt"] <= 2.0 and err["rsqrt"] <= 2.0 and err["div"] <= 2.0, err
+    assert err["sincos_abs"] <= 2e-6, err
+    # the exact mode is the oracle's Mode B, bit for bit
+    s_b, r_b = po.mode_b_roots(x)
+    q_b, _ = po.mode_b_math(x, d)
+    assert got["sqrt", True].tobytes() == s_b.tobytes()
+    assert got["rsqrt", True].tobytes() == r_b.tobytes()
+    assert got["div", True].tobytes() == q_b.tobytes()
+    assert got["sincos", True].tobytes() == po.sincos2pi(m.astype(np.uint32)).tobytes()
+
+
+# ---- images against the reference arithmetic --------------------------------
+
+# (name, W, H, samples per sub-pixel, the absolute bar applies).  synthetic:10000
+# at 64 spp sits above 1e-3 in BOTH modes (measured 1.27e-3: the fp32 flip
+# error falls as 1/sqrt(spp)); C5 is held to the bar at its own 1024 spp in
+# test_gpu_baseline_configs.py
+SCENES = [("simple", 200, 150, 16, True), ("box", 160, 120, 32, True), ("box_mirror", 160, 120, 32, True),
+          ("synthetic:300", 128, 72, 16, True), ("synthetic:10000", 96, 54, 16, False)]
+
+
+@pytest.mark.parametrize("name,W,H,samps,at_bar", SCENES)
+def test_fast_image_vs_reference_arithmetic(name, W, H, samps, at_bar):
+    """RMSE(fast, Mode A/xs) < 1e-3 and no more than the exact mode's own
+    RMSE to Mode A/xs plus a small-frame allowance: both sit at the fp32
+    floor (paths whose discrete decisions flip under rounding)."""
+    _require_gpu()
+    scn = ptgpu.make_scene(name, W, H)
+    cam, sp, ca = _arrays(scn)
+    fast = _image(scn, cam, W, H, samps).astype(np.float64)
+    exact = _image(scn, cam, W, H, samps, flags=EXACT).astype(np.float64)
+    a, _ = po.render_xs_f64(sp, ca, W, H, samps, 2, SEED, nthreads=NT)
+    b, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, nthreads=NT)
+    assert np.array_equal(exact, b.astype(np.float64))
+    rmse = lambda u, v: float(np.sqrt(((u - v) ** 2).mean()))  # noqa: E731
+    r_fast, r_exact, r_fe = rmse(fast, a), rmse(exact, a), rmse(fast, exact)
+    print(f"{name}: fast-vs-A/xs {r_fast:.3e} exact-vs-A/xs {r_exact:.3e} fast-vs-exact {r_fe:.3e}")
+    assert r_fe < NORTH_STAR_RMSE
+    if at_bar:
+        assert r_fast < NORTH_STAR_RMSE, r_fast
+    assert r_fast <= 1.5 * r_exact + 2e-4, (r_fast, r_exact)
+    assert fast.min() >= 0.0 and fast.max() <= 1.0
+
+
+# ---- invariances, GPU against GPU -------------------------------------------
+
+def test_fast_box_frame_invariances():
+    """Bench-size box frame (whole-pixel units + cooperative split tail) in
+    the default mode: equal to the same frame in explicit 3-sample chunks and
+    to its 2-, 4- and 8-way interleaved shards gathered and un-sharded."""
+    _require_gpu()
+    W, H, samps = 1920, 1080, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    full = _image(scn, cam, W, H, samps)
+    assert np.array_equal(full, _image(scn, cam, W, H, samps, chunk=3))
+    with ptgpu.Context(scn, cam) as ctx:
+        for count in (2, 4, 8):
+            rows = ptgpu.shard_rows(H, 1, count)
+            gathered = torch.zeros((count, rows * W * 3), dtype=torch.float32, device="cuda")
+            for k in range(count):
+                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count))
+            image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+            ptgpu.unshard_device(gathered, image, W, H, 1, count)
+            torch.cuda.synchronize()
+            assert np.array_equal(image.cpu().numpy(), full), count
+
+
+@pytest.mark.parametrize("W,H,samps", [(1920, 1080, 8), (1920, 160, 16)])
+def test_fast_bvh_frame_invariances(W, H, samps):
+    """BVH frames in the default mode: the pixel-split tail (1080 rows) and
+    the two unit levels (160 rows) equal explicit 3-sample chunks, and a 3-way
+    shard gathers to the same frame."""
+    _require_gpu()
+    scn = ptgpu.make_scene("synthetic:300", W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    full = _image(scn, cam, W, H, samps)
+    assert np.array_equal(full, _image(scn, cam, W, H, samps, chunk=3))
+    count = 3
+    gathered = torch.from_numpy(np.stack([_image(scn, cam, W, H, samps, rank=k, count=count).reshape(-1)
+                                          for k in range(count)])).cuda()
+    image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    ptgpu.unshard_device(gathered, image, W, H, 1, count)
+    torch.cuda.synchronize()
+    assert np.array_equal(image.cpu().numpy(), full)
+
+
+def test_fast_progressive_passes_equal_one_shot():
+    """Progressive passes in the default mode resolve to the one-shot frame
+    bit for bit; a preview after k samples equals a k-sample frame."""
+    _require_gpu()
+    W, H, samps = 40, 24, 16
+    scn = ptgpu.box_mirror_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    p = ptgpu.make_params(W, H, samps, 2, SEED)
+    rows = ptgpu.shard_rows(H, 8, 1)
+    out = torch.empty(rows * W * 3, dtype=torch.float32, device="cuda")
+    with ptgpu.Context(scn, cam) as ctx:
+        ctx.reset_accumulation(p)
+        done = 0
+        for end in (5, 11, samps):
+            ctx.accumulate(p, done, end)
+            done = end
+            ctx.resolve(out, p, done)
+            torch.cuda.synchronize()
+            prev = out.cpu().numpy().reshape(rows, W, 3)[:H]
+            assert np.array_equal(prev, _image(scn, cam, W, H, done, band_rows=8)), done

@@ -18,6 +18,7 @@ import ptgpu  # noqa: E402
 import pyoracle as po  # noqa: E402
 
 SEED = 0x5EED0001
+EXACT = ptgpu.FLAG_EXACT_MATH
 
 
 def _require_gpu():
@@ -25,28 +26,30 @@ def _require_gpu():
         pytest.fail("gpu tests need a visible MI355X")
 
 
-def _ref(scn, cam, W, H, samps):
+def _ref(scn, cam, W, H, samps, flags):
     img = np.zeros((H * W, 3))
-    ptgpu.render(scn, cam, img, W, H, samps)
+    ptgpu.render(scn, cam, img, W, H, samps, flags=flags)
     return img
 
 
+@pytest.mark.parametrize("mode", [pytest.param(EXACT, id="exact"), pytest.param(0, id="fast")])
 @pytest.mark.parametrize("local", [0, 2, 3, 8])
-def test_multi_context_frames_and_progressive_passes(local):
+def test_multi_context_frames_and_progressive_passes(local, mode):
     """A persistent context: two frames add into the image like ptg_render
     (image[row] += ..., main.cpp:196), frames of another size reuse it, and
     progressive passes over all shards resolve to the one-shot image bit for
-    bit (previews equal the oracle at that sample count)."""
+    bit -- in both arithmetic modes (exact: previews and frames equal the
+    oracle at that sample count)."""
     _require_gpu()
     W, H, samps = 52, 30, 8
     scn = ptgpu.box_mirror_scene(W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     sp = np.ascontiguousarray(scn.to_array().view(po.SPHERE_DT))
     ca = np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT))
-    ref = _ref(scn, cam, W, H, samps)
+    ref = _ref(scn, cam, W, H, samps, mode)
     with ptgpu.MultiContext(scn, cam, [0], local_shards=local) as m:
         for br in (1, 4, 7):
-            p = ptgpu.make_params(W, H, samps, 2, SEED, br)
+            p = ptgpu.make_params(W, H, samps, 2, SEED, br, flags=mode)
             img = np.zeros((H * W, 3))
             m.render(img, p)
             assert np.array_equal(img, ref), br
@@ -54,12 +57,15 @@ def test_multi_context_frames_and_progressive_passes(local):
             assert np.array_equal(img, 2.0 * ref), br
         # a smaller frame on the same context (same scene: the camera's aspect
         # is the scene's, the image size is the params')
-        p2 = ptgpu.make_params(W // 2, H // 2, samps, 2, SEED, 1)
+        p2 = ptgpu.make_params(W // 2, H // 2, samps, 2, SEED, 1, flags=mode)
         img2 = np.zeros((H // 2 * (W // 2), 3))
         m.render(img2, p2)
         b, _ = po.render_xs_f32(sp, ca, W // 2, H // 2, samps, 2, SEED)
-        assert np.array_equal(img2.reshape(H // 2, W // 2, 3), b.astype(np.float64))
-        p = ptgpu.make_params(W, H, samps, 2, SEED, 2)
+        if mode == EXACT:
+            assert np.array_equal(img2.reshape(H // 2, W // 2, 3), b.astype(np.float64))
+        else:
+            assert np.array_equal(img2, _ref(scn, cam, W // 2, H // 2, samps, mode))
+        p = ptgpu.make_params(W, H, samps, 2, SEED, 2, flags=mode)
         m.reset_accumulation(p)
         done = 0
         prev = np.zeros((H, W, 3), dtype=np.float32)
@@ -67,8 +73,9 @@ def test_multi_context_frames_and_progressive_passes(local):
             m.accumulate(p, done, end)
             done = end
             m.resolve(prev, p, done)
-            b, _ = po.render_xs_f32(sp, ca, W, H, done, 2, SEED)
-            assert np.array_equal(prev, b), done
+            if mode == EXACT:
+                b, _ = po.render_xs_f32(sp, ca, W, H, done, 2, SEED)
+                assert np.array_equal(prev, b), done
         assert np.array_equal(prev.astype(np.float64).reshape(H * W, 3), ref)
 
 
@@ -114,7 +121,7 @@ def test_partial_pixel_group_with_the_largest_chunk():
     ca = np.ascontiguousarray(cam.to_array().view(po.CAMERA_DT))
     out = torch.full((W * H * 3,), -7.0, dtype=torch.float32, device="cuda")
     with ptgpu.Context(scn, cam) as ctx:
-        ctx.render_device(out, ptgpu.make_params(W, H, samps, nsub, SEED, chunk_samples=1 << 20))
+        ctx.render_device(out, ptgpu.make_params(W, H, samps, nsub, SEED, chunk_samples=1 << 20, flags=EXACT))
         torch.cuda.synchronize()
     gpu = out.cpu().numpy().reshape(H, W, 3)
     b, _ = po.render_xs_rect(sp, ca, W, H, samps, nsub, SEED, nthreads=16)

@@ -1,8 +1,13 @@
 """GPU parity: the HIP megakernel (through the C ABI) against the oracle.
 
-Tolerance: the kernel and the oracle's Mode B execute the same fp32 op
-sequence, so the bar is BIT-EXACT equality (max |diff| == 0) of images,
-per-path radiance and segment counts.  The north-star tolerance (per-pixel
+Tolerance: in its exact arithmetic mode (PTG_FLAG_EXACT_MATH) the kernel and
+the oracle's Mode B execute the same fp32 op sequence, so the bar is
+BIT-EXACT equality (max |diff| == 0) of images, per-path radiance and segment
+counts.  The default (fast-transcendental) mode is held to the north star's
+RMSE against the reference arithmetic in test_gpu_reference.py and
+test_gpu_baseline_configs.py, and to the same GPU-vs-GPU invariances
+(shards, work units, split tails, progressive passes) bit for bit in
+test_gpu_fast_math.py.  The north-star tolerance (per-pixel
 RMSE < 1e-3 on the float image, post-clamp, pre-gamma) is asserted as well
 so that a future non-bit-exact kernel change fails loudly on the stated bar.
 """
@@ -17,6 +22,7 @@ import pyoracle as po  # noqa: E402
 
 RMSE_TOL = 1e-3
 SEED = 0x5EED0001
+EXACT = ptgpu.FLAG_EXACT_MATH  # every image here is compared with Mode B bit for bit
 
 
 def _require_gpu():
@@ -35,7 +41,7 @@ def _oracle_scene(scn, cam):
 def _gpu_image(scn, cam, W, H, samps, nsub=2, seed=SEED, band_rows=8, rank=0, count=1, count_segments=False,
                chunk=0):
     p = ptgpu.make_params(W, H, samps, nsub, seed, band_rows, rank, count, chunk,
-                          flags=ptgpu.FLAG_COUNT_TESTS if count_segments else 0)
+                          flags=(ptgpu.FLAG_COUNT_TESTS if count_segments else 0) | EXACT)
     rows = ptgpu.shard_rows(H, band_rows, count)
     out = torch.full((rows * W * 3,), -7.0, dtype=torch.float32, device="cuda")
     segs = torch.zeros(3, dtype=torch.int64, device="cuda") if count_segments else None
@@ -212,7 +218,7 @@ def test_per_path_radiance_bitexact(name):
     n = 1500
     coords = np.stack([rng.integers(0, W, n), rng.integers(0, H, n), rng.integers(0, 2, n),
                        rng.integers(0, 2, n), rng.integers(0, 1 << 20, n)], axis=1).astype(np.int32)
-    p = ptgpu.make_params(W, H, 1, 2, SEED)
+    p = ptgpu.make_params(W, H, 1, 2, SEED, flags=EXACT)
     with ptgpu.Context(scn, cam) as ctx:
         out, segs = ctx.trace_samples(torch.from_numpy(coords).cuda(), p)
     out = out.cpu().numpy()
@@ -271,11 +277,11 @@ def test_drop_in_render_adds_into_double_image():
     scn = ptgpu.box_mirror_scene(W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     img = np.zeros((H * W, 3), dtype=np.float64)
-    ptgpu.render(scn, cam, img, W, H, samps)
+    ptgpu.render(scn, cam, img, W, H, samps, flags=EXACT)
     sp, ca = _oracle_scene(scn, cam)
     ref, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED)
     assert np.array_equal(img.reshape(H, W, 3), ref.astype(np.float64))
-    ptgpu.render(scn, cam, img, W, H, samps)  # accumulates like image[row] += (main.cpp:196)
+    ptgpu.render(scn, cam, img, W, H, samps, flags=EXACT)  # accumulates like image[row] += (main.cpp:196)
     assert np.array_equal(img.reshape(H, W, 3), 2.0 * ref.astype(np.float64))
 
 
@@ -293,7 +299,7 @@ def test_shard_invariance_full_size():
     gathered = torch.zeros((count, rows * W * 3), dtype=torch.float32, device="cuda")
     with ptgpu.Context(scn, cam) as ctx:
         for k in range(count):
-            ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, br, k, count))
+            ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, br, k, count, flags=EXACT))
         image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
         ptgpu.unshard_device(gathered, image, W, H, br, count)
         torch.cuda.synchronize()
@@ -337,9 +343,9 @@ def test_invalid_arguments_fail_loudly():
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     img = np.zeros((64, 3))
     with pytest.raises(ptgpu.PtgError):
-        ptgpu.render(scn, cam, img, 8, 8, 4, num_subpixels=9)
+        ptgpu.render(scn, cam, img, 8, 8, 4, num_subpixels=9, flags=EXACT)
     with pytest.raises(ptgpu.PtgError):
-        ptgpu.render(scn, cam, img, 8, 8, -1)
+        ptgpu.render(scn, cam, img, 8, 8, -1, flags=EXACT)
 
 
 def test_progressive_accumulation_matches_one_shot():
@@ -350,7 +356,7 @@ def test_progressive_accumulation_matches_one_shot():
     W, H, samps = 40, 24, 16
     scn = ptgpu.box_scene(W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
-    p = ptgpu.make_params(W, H, samps, 2, SEED)
+    p = ptgpu.make_params(W, H, samps, 2, SEED, flags=EXACT)
     rows = ptgpu.shard_rows(H, 8, 1)
     out = torch.empty(rows * W * 3, dtype=torch.float32, device="cuda")
     sp, ca = _oracle_scene(scn, cam)
@@ -411,7 +417,7 @@ def test_cli_renders_and_splits_over_devices(tmp_path):
     assert outs["0"].startswith(header)
     scn = ptgpu.box_scene(W, H)
     img = np.zeros((H * W, 3))
-    ptgpu.render(scn, ptgpu.camera.with_config(scn.camera_parameters), img, W, H, spp // 4)
+    ptgpu.render(scn, ptgpu.camera.with_config(scn.camera_parameters), img, W, H, spp // 4)  # the CLI's default mode
     ref = po.tonemap(img).astype(np.uint8).tobytes()
     assert outs["0"][len(header):] == ref
 
@@ -450,7 +456,7 @@ def test_shards_with_split_tail_are_exact():
             rows = ptgpu.shard_rows(H, 1, count)
             gathered = torch.zeros((count, rows * W * 3), dtype=torch.float32, device="cuda")
             for k in range(count):
-                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count))
+                ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count, flags=EXACT))
             image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
             ptgpu.unshard_device(gathered, image, W, H, 1, count)
             torch.cuda.synchronize()
@@ -490,12 +496,12 @@ def test_render_multi_rccl_one_rank_is_exact():
     scn = ptgpu.box_mirror_scene(W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     ref = np.zeros((H * W, 3))
-    ptgpu.render(scn, cam, ref, W, H, samps)
+    ptgpu.render(scn, cam, ref, W, H, samps, flags=EXACT)
     # each call is a fresh context on a non-blocking stream (its first frame
     # once raced a null-stream zeroing of the accumulator: ensure_acc)
     for br in (1, 4, 2, 8, 4):
         img = np.zeros((H * W, 3))
-        ptgpu.render_multi(scn, cam, img, W, H, samps, [0], band_rows=br)
+        ptgpu.render_multi(scn, cam, img, W, H, samps, [0], band_rows=br, flags=EXACT)
         assert np.array_equal(img, ref), br
     with pytest.raises(ptgpu.PtgError, match="distinct devices"):
         ptgpu.render_multi(scn, cam, np.zeros((H * W, 3)), W, H, samps, [0, 0])
@@ -520,7 +526,7 @@ def test_render_sharded_on_nccl_backend():
                             device_id=torch.device("cuda", 0))
     try:
         assert dist.get_backend() == "nccl"
-        p = ptgpu.make_params(W, H, samps, 2, SEED, 1, 0, 1)
+        p = ptgpu.make_params(W, H, samps, 2, SEED, 1, 0, 1, flags=EXACT)
         slab = torch.zeros(ptgpu.shard_rows(H, 1, 1) * W * 3, dtype=torch.float32, device="cuda")
         with ptgpu.Context(scn, cam) as ctx:
             image = ptgpu.render_sharded(p, slab, ctx=ctx)
@@ -545,7 +551,7 @@ def test_c4_frame_size_shards_are_exact():
     gathered = torch.zeros((count, rows * W * 3), dtype=torch.float32, device="cuda")
     with ptgpu.Context(scn, cam) as ctx:
         for k in range(count):
-            ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count))
+            ctx.render_device(gathered[k], ptgpu.make_params(W, H, samps, 2, SEED, 1, k, count, flags=EXACT))
         image = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
         ptgpu.unshard_device(gathered, image, W, H, 1, count)
         torch.cuda.synchronize()
