@@ -167,6 +167,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BOX_MODE
 #define PTG_BOX_MODE 1  // linear scenes: nearest-plane wall first (box mode, scene_scan)
 #endif
+#ifndef PTG_LEAF_SEL
+#define PTG_LEAF_SEL 0  // A/B: the fast mode's leaf sphere test as straight-line selects
+#endif
+#ifndef PTG_BVH_LDS_ROOT
+#define PTG_BVH_LDS_ROOT 0  // A/B: the root wide node of every octant layout read from LDS
+#endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
                           // (measured with octant layouts + SAH: 6 beats 4 by 7 %, 5 and 7 by 1-2 %)
@@ -713,6 +719,18 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
         disc = __builtin_fmaf(a, -g0.w, -dot3(x, x));
         disc = c >= 0.0f ? __builtin_fminf(disc, hb * hb) : disc;
     }
+#if PTG_LEAF_SEL
+    if constexpr (!kExact) {  // A/B: straight-line selects (the fast sqrt and division are cheap)
+        const float sq = Math<false>::sqrt0(disc);
+        const bool neg = hb < 0.0f;
+        const float qq = sq + __builtin_fabsf(hb);
+        const bool near_lt = c < kEps * qq;
+        const float num = neg ? (near_lt ? qq : c) : -c;
+        const float den = (neg & near_lt) ? a : qq;
+        const float t = Math<false>::div(num, den);
+        return (behind | beyond | (disc < 0.0f) | (num < kEps * den)) ? kReject : t;
+    }
+#endif
     if (behind | beyond | (disc < 0.0f))
         return kReject;
     const float sq = Math<kExact>::sqrt(disc);  // disc >= 0 here
@@ -918,11 +936,27 @@ __device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, 
 constexpr int kPopLater = -2;
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
-                                              ScanCount &cnt)
+                                              ScanCount &cnt, const u32x4 *lds_root = nullptr, int root_mask = 0,
+                                              int shift = 0)
 {
     const int base = tr.ni & ~3;
-    gptr<u32x4> q = qnodes + base;
-    const u32x4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    u32x4 q0, q1, q2, q3;
+#if PTG_BVH_LDS_ROOT
+    if (lds_root && (base & root_mask) == 0) {  // a layout's root: staged in LDS
+        const u32x4 *l = lds_root + ((base >> shift) << 2);
+        q0 = l[0];
+        q1 = l[1];
+        q2 = l[2];
+        q3 = l[3];
+    } else
+#endif
+    {
+        gptr<u32x4> q = qnodes + base;
+        q0 = q[0];
+        q1 = q[1];
+        q2 = q[2];
+        q3 = q[3];
+    }
     if constexpr (kCount)
         cnt.boxes += 4 - (tr.ni & 3);
     const float tcap = tr.tb * 1.0001f;
@@ -1705,6 +1739,17 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
 #if PTG_LEAF_SPLIT
         __shared__ uint8_t lds_pair[kWaves][2][64];  // leaf phase: owner / helper lane of each rank
 #endif
+#if PTG_BVH_LDS_ROOT
+        // the 8 octant layouts' root nodes (4 records each), 512 B
+        __shared__ u32x4 lds_root[8][4];
+        int root_shift = A.bvh_shift;
+        asm volatile("" : "+s"(root_shift));
+        const int root_mask = (1 << root_shift) - 1;
+        if (A.n_nodes > 0 && lane < 32)
+            lds_root[lane >> 2][lane & 3] = ((gptr<u32x4>)A.bvh_qnodes)[((lane >> 2) << root_shift) + (lane & 3)];
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+#endif
         // kernel-argument pointers used in the loops, pinned in SGPRs once:
         // left to the compiler they were re-loaded (s_load + wait) in every
         // node step and every shade
@@ -1769,7 +1814,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         // (the node step as selects for the whole wave, like the
                         // leaf completion: +2.3 % -- its loads and selects for idle lanes)
                         if (trv && tr.pend < 0)
+#if PTG_BVH_LDS_ROOT
+                            bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt, &lds_root[0][0],
+                                                                     root_mask, root_shift);
+#else
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
+#endif
                         PTG_PHASE(1);
                         phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
                     }

@@ -12,7 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "cpu-path-tracing_amd", "csrc", "ptg_render.hip")
-KERNEL = "_ZN12_GLOBAL__N_113render_kernelILb0ELb0EEEvNS_5KArgsE"
+KERNEL = os.environ.get("ISA_KERNEL", "_ZN12_GLOBAL__N_113render_kernelILb0ELb0ELb0EEEvNS_5KArgsE")  # <kCount, kBvh, kExact>: the default (fast) linear kernel
 
 
 def compile_asm(defs):
