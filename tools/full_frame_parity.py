@@ -54,7 +54,10 @@ def main():
     out = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda:0")
     t0 = time.perf_counter()
     with ptgpu.Context(scn, cam, device=0) as ctx:
-        ctx.render_device(out, ptgpu.make_params(W, H, samps, nsub, seed))
+        # the exact arithmetic mode: the image compared with Mode B bit for bit
+        # (FFP_MODE=fast: the default mode, held to the RMSE columns only)
+        flags = 0 if os.environ.get("FFP_MODE") == "fast" else ptgpu.FLAG_EXACT_MATH
+        ctx.render_device(out, ptgpu.make_params(W, H, samps, nsub, seed, flags=flags))
         torch.cuda.synchronize()
     t_gpu = time.perf_counter() - t0
     gpu = out.cpu().numpy().reshape(rows, W, 3)[:H].astype(np.float64)
