@@ -167,20 +167,8 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BOX_MODE
 #define PTG_BOX_MODE 1  // linear scenes: nearest-plane wall first (box mode, scene_scan)
 #endif
-#ifndef PTG_LEAF_SEL
-#define PTG_LEAF_SEL 0  // A/B: the fast mode's leaf sphere test as straight-line selects
-#endif
 #ifndef PTG_BVH_LDS_ROOT
 #define PTG_BVH_LDS_ROOT 0  // A/B: the root wide node of every octant layout read from LDS
-#endif
-#ifndef PTG_SMALL_PREFETCH
-#define PTG_SMALL_PREFETCH 0  // A/B: linear scan, the next small sphere's record read during the current test
-#endif
-#ifndef PTG_SMALL_UNROLL
-#define PTG_SMALL_UNROLL 0  // A/B: unroll the small-sphere loop
-#endif
-#ifndef PTG_WALL_SGPR
-#define PTG_WALL_SGPR 0  // A/B: box mode's nearest wall record offset selected from SGPR values (no LDS table read)
 #endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
@@ -414,26 +402,12 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     const LinRec *best = recs + A.n;
-#if PTG_SMALL_PREFETCH
-    float4 pre0 = {}, pre1 = {};  // the small sphere's record, read one iteration ahead
-#endif
     auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
                         const bool valid = true, const int ks = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
         // r is wave-uniform, except for a pair's walls / box mode
-#if PTG_SMALL_PREFETCH
-        float4 g0, g1;
-        if constexpr (kKind == kSmall) {
-            g0 = pre0;
-            g1 = pre1;
-        } else {
-            g0 = r->g.g0;
-            g1 = r->g.g1;
-        }
-#else
         float4 g0 = r->g.g0;
         float4 g1 = r->g.g1;
-#endif
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
         float ed = dot3(e, d);
         float ee = dot3(e, e);
@@ -557,9 +531,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // k's + wall (2k) and - wall (2k + 1), -1 where missing
         const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
         float u[3], v[3];
-#if PTG_WALL_SGPR
-        int tow[3];  // per axis the record offset of the wall the ray moves toward (-1: none)
-#endif
         for (int k = 0; k < 3; ++k) {
             // the uniform plane / record values stay in SGPRs: select values,
             // not kernel-argument addresses (that became per-lane loads)
@@ -567,11 +538,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             asm volatile("" : "+s"(pp), "+s"(pm));
             const float dk = comp(d, k);
             const bool pos = dk >= 0.0f;
-#if PTG_WALL_SGPR
-            int rp = A.rec_plus[k], rm = A.rec_minus[k];
-            asm volatile("" : "+s"(rp), "+s"(rm));
-            tow[k] = pos ? rp : rm;
-#endif
+
             // (o - pm) is the same IEEE subtraction as -(pm - o).  A missing
             // wall's plane is at +-inf: u = inf is never the nearest (inf * v
             // is inf or NaN, and NaN compares false) and never needed below
@@ -581,24 +548,16 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         }
         float un = u[0], vn = v[0];
         int kn = 0;
-#if PTG_WALL_SGPR
-        int in = tow[0];
-#endif
         for (int k = 1; k < 3; ++k) {
             const bool nearer = u[k] * vn < un * v[k];
             un = nearer ? u[k] : un;
             vn = nearer ? v[k] : vn;
             kn = nearer ? k : kn;
-#if PTG_WALL_SGPR
-            in = nearer ? tow[k] : in;
-#endif
         }
         // kn's wall is missing only when no existing wall the ray moves
         // toward has v > 0 (every such plane is parallel to the ray): then no
         // wall can be hit from inside the room, and the test is masked
-#if !PTG_WALL_SGPR
         const int in = walls[2 * kn + (comp(d, kn) >= 0.0f ? 0 : 1)];
-#endif
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, kAxAny>{}, un, vn, in >= 0);
         const float bqm = bq * kPlaneMargin;
@@ -705,29 +664,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     }
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
-#if PTG_SMALL_PREFETCH
-    if (i < A.n) {
-        pre0 = recs[i].g.g0;
-        pre1 = recs[i].g.g1;
-    }
-    for (; i < A.n; ++i) {
-        const float4 c0 = pre0, c1 = pre1;
-        const int j = i + 1 < A.n ? i + 1 : i;
-        const float4 n0 = recs[j].g.g0, n1 = recs[j].g.g1;
-        pre0 = c0;
-        pre1 = c1;
-        test(i, std::integral_constant<int, kSmall>{});
-        pre0 = n0;
-        pre1 = n1;
-    }
-#elif PTG_SMALL_UNROLL
-#pragma unroll PTG_SMALL_UNROLL
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
-#else
-    for (; i < A.n; ++i)
-        test(i, std::integral_constant<int, kSmall>{});
-#endif
     tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
     return best;
 }
@@ -779,18 +717,6 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
         disc = __builtin_fmaf(a, -g0.w, -dot3(x, x));
         disc = c >= 0.0f ? __builtin_fminf(disc, hb * hb) : disc;
     }
-#if PTG_LEAF_SEL
-    if constexpr (!kExact) {  // A/B: straight-line selects (the fast sqrt and division are cheap)
-        const float sq = Math<false>::sqrt0(disc);
-        const bool neg = hb < 0.0f;
-        const float qq = sq + __builtin_fabsf(hb);
-        const bool near_lt = c < kEps * qq;
-        const float num = neg ? (near_lt ? qq : c) : -c;
-        const float den = (neg & near_lt) ? a : qq;
-        const float t = Math<false>::div(num, den);
-        return (behind | beyond | (disc < 0.0f) | (num < kEps * den)) ? kReject : t;
-    }
-#endif
     if (behind | beyond | (disc < 0.0f))
         return kReject;
     const float sq = Math<kExact>::sqrt(disc);  // disc >= 0 here
@@ -1818,7 +1744,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         gptr<int> cont = (gptr<int>)A.bvh_cont;
         asm volatile("" : "+s"(cont));
 #if !PTG_NO_TRIG_PIN
-        asm volatile("" : "+s"(trig));
+        if constexpr (kExact)  // (the fast mode's sin/cos read no table)
+            asm volatile("" : "+s"(trig));
 #endif
 #if PTG_BVH_WIDE
         const int oct_mask = 7;  // every octant has its layout
