@@ -420,6 +420,14 @@ def test_cli_renders_and_splits_over_devices(tmp_path):
     ptgpu.render(scn, ptgpu.camera.with_config(scn.camera_parameters), img, W, H, spp // 4)  # the CLI's default mode
     ref = po.tonemap(img).astype(np.uint8).tobytes()
     assert outs["0"][len(header):] == ref
+    # --exact-math: the bytes of the CPU oracle's image (Mode B, color_to_int)
+    out = tmp_path / "img_exact.ppm"
+    r = subprocess.run([cli, "--scene", "box", "--width", str(W), "--height", str(H), "--spp", str(spp), "--format",
+                        "p6", "--exact-math", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    sp, ca = _oracle_scene(scn, ptgpu.camera.with_config(scn.camera_parameters))
+    b, _ = po.render_xs_f32(sp, ca, W, H, spp // 4, 2, ptgpu.DEFAULT_SEED)
+    assert out.read_bytes()[len(header):] == po.tonemap(b.astype(np.float64)).astype(np.uint8).tobytes()
 
 
 def test_split_tail_frame_is_exact():
