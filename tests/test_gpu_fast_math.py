@@ -213,3 +213,27 @@ def test_fast_progressive_passes_equal_one_shot():
             torch.cuda.synchronize()
             prev = out.cpu().numpy().reshape(rows, W, 3)[:H]
             assert np.array_equal(prev, _image(scn, cam, W, H, done, band_rows=8)), done
+
+
+@pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300", "synthetic:10000"])
+def test_fast_no_out_of_range_radiance(name):
+    """PTG_FLAG_COUNT_NONFINITE in the default mode: no path of the shipped
+    scenes has a NaN, negative or > 2^30 radiance component (the exact
+    accumulation would clip it), and the segment count is within 0.1 % of
+    the exact mode's (the same paths up to rounding-level flips)."""
+    _require_gpu()
+    W, H, samps = 96, 64, 16
+    scn = ptgpu.make_scene(name, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    res = {}
+    for mode in (0, EXACT):
+        cnt = torch.zeros(4, dtype=torch.int64, device="cuda")
+        out = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
+        with ptgpu.Context(scn, cam) as ctx:
+            ctx.render_device(out, ptgpu.make_params(W, H, samps, 2, SEED, 1,
+                                                     flags=mode | ptgpu.FLAG_COUNT_TESTS | ptgpu.FLAG_COUNT_NONFINITE),
+                              cnt)
+            torch.cuda.synchronize()
+        res[mode] = [int(v) for v in cnt.cpu().tolist()]
+    assert res[0][3] == 0 and res[EXACT][3] == 0, res
+    assert abs(res[0][0] - res[EXACT][0]) <= 1e-3 * res[EXACT][0], res
