@@ -17,9 +17,13 @@
  *   Mode A / xs : double, reference arithmetic, counter-based xorshift32 draws
  *                 keyed by (seed, pixel, sub-pixel, sample) instead of a
  *                 per-row mt19937 (the RNG swap the north star asks for).
- *   Mode B / xs : float, the op sequence the GPU kernel executes (explicit
- *                 fmaf, IEEE div/sqrt, own sin/cos polynomial, anchored
- *                 quadratic for huge spheres).  The GPU image must equal it.
+ *   Mode B / xs : float, the op sequence the GPU kernel executes in its
+ *                 exact arithmetic mode (PTG_FLAG_EXACT_MATH: explicit fmaf,
+ *                 deterministic div/sqrt/rsqrt sequences, table sin/cos,
+ *                 anchored quadratic for huge spheres).  The exact-mode GPU
+ *                 image must equal it bit for bit; the default mode (the
+ *                 GPU's v_sqrt/v_rsq/v_rcp/v_sin/v_cos) is held to the
+ *                 RMSE bar against Mode A/xs instead.
  *
  * Parity status: L0 (vec/ray/sphere/hit_record/camera/random_state/utils) is
  * pinned against the compiled reference; main.cpp (radiance, BRDFs,
