@@ -125,6 +125,13 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // of that frame, 2-4 rounds, keep 8)
 #define PTG_TAIL_CHUNKS_MANY 4
 #endif
+#ifndef PTG_BVH_TAIL_CHUNKS_MANY
+// ... and for BVH scenes, whose pixel-split tail units carry every sample of
+// their pixels (no HBM accumulation either way): 8 units of 2 pixels per
+// group (C5 -0.85 % against 4, A/B 244.4-244.7 vs 246.3-247.1 ms; the box
+// scenes keep 4, the cooperative LDS-reduced level)
+#define PTG_BVH_TAIL_CHUNKS_MANY 8
+#endif
 #ifndef PTG_TAIL_MIN_HALF_ROUNDS
 // linear scenes: split tail from 1.5 rounds of wave slots on (measured with
 // tools/shard_sim.py: 2/4/8-way shards of the bench frame 1.6/1.8/1.4 %
@@ -2482,7 +2489,8 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
         constexpr int kLinWaves = kBlock / 64;
         for (; l <= PTG_TAIL_LEVELS && rows_left > 0; ++l) {
             const int rows = l == PTG_TAIL_LEVELS ? rows_left : (rows_left + 1) / 2;
-            const int tc = (many ? PTG_TAIL_CHUNKS_MANY : PTG_TAIL_CHUNKS) << (l - 1);
+            const int tc = (many ? (ctx->n > kLinearMax ? PTG_BVH_TAIL_CHUNKS_MANY : PTG_TAIL_CHUNKS_MANY)
+                                 : PTG_TAIL_CHUNKS) << (l - 1);
             const int ch = (nsamp + tc - 1) / tc;
             const int nch = (nsamp + ch - 1) / ch;
             // one chunk per wave of a (linear-kernel) workgroup: the level's
