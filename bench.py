@@ -14,16 +14,39 @@ t1_ms and efficiency = T1 / (N * T_N) of this run, so the scaling line is
 self-contained (the N = 1 default line is the metric's 1080p frame).
 --workload c1..c5 / bench pick one config for every N.
 
+Launch modes (resolve_launch):
+  * WORLD_SIZE unset, --gpus 1           one GPU.
+  * WORLD_SIZE unset, --gpus N > 1       ONE process drives GPUs 0..N-1
+                                         through ptg_multi (csrc/ptg_multi.cpp):
+                                         N shards, ONE ncclGather (RCCL over
+                                         xGMI, communicators from
+                                         ncclCommInitAll), the un-shard on GPU 0
+                                         -- no launcher needed.
+  * WORLD_SIZE = N (torchrun)            one process per GPU, torch.distributed
+                                         on nccl (RCCL); the gather is
+                                         ptgpu.render_sharded's.
+  * WORLD_SIZE set and != --gpus         an error (exit 2): the line would
+                                         otherwise claim a GPU count it did not
+                                         measure.
+PTG_REHEARSAL=1 runs either N > 1 mode on one GPU (N shards on device 0; gloo
+for torchrun) -- a 1-GPU box rehearsal of the sharded path, labelled as such.
+Efficiency = T1 / (N * T_N) with T1 and T_N timed the same way: wall clock
+per frame over the same kind of step (render + gather + un-shard), and again
+from the kernels' HIP events alone (efficiency_kernel).
+
 Also reported:
   roofline     -- VALU fp32 roofline of the render kernel: algorithmic FLOP
                   per launch (S_bar*(23*N_spheres + 100) + 60 per sample,
                   SURVEY.md 8(d), S_bar measured by the kernel's own segment
                   counter) / its average launch time from HIP events on the
                   launch stream; peak 157.3 TFLOP/s (MI355X fp32 vector).
-  cpu_baseline -- the repo's own OpenMP CPU loop (oracle/, the reference
-                  algorithm in double + mt19937, "port") on a bounded sample
-                  of the same workload, rank 0 at N=1 only; with the quality
-                  rows of the benchmarked frame against the oracle.
+  cpu_baseline -- the REFERENCE's own per-pixel code (src/main.cpp:27-197
+                  compiled with its `pt` library into oracle/_ref/libref_main.so,
+                  kind "reference") in an OpenMP row loop on the host's cores,
+                  on a bounded sample of the same workload, rank 0 at N=1 only;
+                  beside it the repo's C restatement (oracle Mode A, "port") on
+                  the same sample, and the quality rows of the benchmarked frame
+                  against the oracle.
 
 Arithmetic: the default (product) mode takes square roots, reciprocal
 square roots, the hit division and sin/cos from the GPU's transcendental
@@ -105,9 +128,15 @@ def default_cpu_threads():
 
 
 def cpu_baseline(scene_name, W, H, samps, nsub, threads, row_step, gpu_image=None, seed=None, quality_rows=4):
-    """Time the repo's OpenMP CPU path (oracle Mode A: reference arithmetic,
-    double + mt19937 row seeding) on every row_step-th row of the frame, all
-    samples of those rows; the rate extrapolates linearly to the frame.
+    """Time the reference's own per-pixel code on the host: every row_step-th
+    row of the frame, all samples of those rows, in an OpenMP
+    schedule(dynamic,1) row loop (main.cpp:217-234's task body, per-row
+    mt19937(RD * (unsigned short)(y^3)) with RD = 1 for random_device); the
+    rate extrapolates linearly to the frame.  kind "reference" when
+    oracle/_ref/libref_main.so was built (the reference compiled in this
+    container, shipped with the tree), else the restatement ("port").  The
+    port (oracle Mode A: the same algorithm restated in C, same seeds) is
+    timed on the same rows beside it.
 
     With `gpu_image` (the benchmarked frame, [H, W, 3] float32) the same leg
     also checks quality on `quality_rows` evenly spaced rows:
@@ -123,27 +152,53 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, row_step, gpu_image=Non
     except Exception as e:  # noqa: BLE001
         log(f"cpu_baseline unavailable: {e}")
         return None
+    pr = None
+    try:
+        import pyref
+        if pyref.available():
+            pyref.lib()
+            pr = pyref
+        else:
+            log("cpu_baseline: oracle/_ref/libref_main.so not built; timing the port only")
+    except Exception as e:  # noqa: BLE001
+        log(f"cpu_baseline: reference build unusable ({e}); timing the port only")
     scn = ptgpu.make_scene(scene_name, W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     sp = scn.to_array().view(po.SPHERE_DT)
     ca = cam.to_array().view(po.CAMERA_DT)
-    img = np.zeros(W * H * 3)
     rows = len(range(0, H, row_step))
-    t0 = time.perf_counter()
-    rc = po.lib().po_render_mt(po.ptr(sp), len(sp), po.ptr(ca), W, H, samps, nsub, 1, 0, H, row_step, threads,
-                               po.ptr(img))
-    assert rc == 0
-    dt = time.perf_counter() - t0
     nsamp = rows * W * samps * nsub * nsub
-    rate = nsamp / dt
-    out = {"value": round(rate / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "port",
-           "seconds": round(dt, 2),
-           "frame_seconds_extrapolated": round(W * H * samps * nsub * nsub / rate, 1),
-           "host": host_cpu_info(),
-           "sample": (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp: every {row_step}th row ({rows} of {H}, "
-                      f"all their samples) timed, the frame extrapolated linearly; oracle Mode A (double, mt19937 "
-                      f"per row, reference arithmetic) in an OpenMP schedule(dynamic,1) row loop on {threads} "
-                      f"threads")}
+    sample = (f"{scene_name} {W}x{H} at {samps * nsub * nsub} spp: every {row_step}th row ({rows} of {H}, all "
+              f"their samples) timed, the frame extrapolated linearly; OpenMP schedule(dynamic,1) row loop on "
+              f"{threads} threads, per-row mt19937(1 * (unsigned short)(y^3)) (main.cpp:222-223)")
+
+    def timed(fn):
+        t0 = time.perf_counter()
+        fn()
+        return time.perf_counter() - t0
+
+    img = np.zeros(W * H * 3)
+    dt_port = timed(lambda: po.lib().po_render_mt(po.ptr(sp), len(sp), po.ptr(ca), W, H, samps, nsub, 1, 0, H,
+                                                   row_step, threads, po.ptr(img)))
+    port = {"value": round(nsamp / dt_port / 1e6, 4), "seconds": round(dt_port, 2),
+            "what": "oracle Mode A (oracle/pt_oracle.c: main.cpp:30-197 restated in C, double + mt19937)"}
+    if pr is not None:
+        ref_img = np.zeros(W * H * 3)
+        seeds = pr.reference_row_seeds(H, 1)
+        dt = timed(lambda: pr.render_rows(sp, ca, W, H, samps, nsub, seeds, rows=(0, H, row_step), nthreads=threads,
+                                          image=ref_img))
+        same = bool(np.array_equal(ref_img, img))
+        out = {"value": round(nsamp / dt / 1e6, 4), "unit": "Mray-samples/s", "cores": threads, "kind": "reference",
+               "seconds": round(dt, 2), "frame_seconds_extrapolated": round(W * H * samps * nsub * nsub * dt / nsamp, 1),
+               "sample": sample + "; the reference's src/main.cpp:27-197 + `pt` library (-O3) via "
+                                  "oracle/_ref/libref_main.so",
+               "port": dict(port, image_equals_reference=same)}
+    else:
+        out = {"value": port["value"], "unit": "Mray-samples/s", "cores": threads, "kind": "port",
+               "seconds": port["seconds"],
+               "frame_seconds_extrapolated": round(W * H * samps * nsub * nsub * dt_port / nsamp, 1),
+               "sample": sample + "; " + port["what"]}
+    out["host"] = host_cpu_info()
     if gpu_image is not None and quality_rows > 0:
         step_y = max(1, H // quality_rows)
         ys = np.arange(step_y // 2, H, step_y)[:quality_rows]  # image-space y (main.cpp:181: y = 0 at the bottom)
@@ -165,6 +220,25 @@ def cpu_baseline(scene_name, W, H, samps, nsub, threads, row_step, gpu_image=Non
     return out
 
 
+def resolve_launch(gpus, env):
+    """(mode, world, rank, local) for --gpus and the launcher's environment:
+    "single" (one GPU), "inprocess" (no launcher, --gpus N > 1: one process,
+    ptg_multi over GPUs 0..N-1) or "torchrun" (WORLD_SIZE ranks).  A
+    WORLD_SIZE that disagrees with --gpus raises ValueError."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return ("inprocess" if gpus > 1 else "single"), 1, 0, 0
+    world = int(ws)
+    if world != gpus:
+        raise ValueError(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks: the line would "
+                         f"report a GPU count it did not measure")
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", "0"))
+    return ("torchrun" if world > 1 else "single"), world, rank, local
+
+
 def load_pmc(workload):
     """PMC figures of the committed rocprofv3 profile of this workload
     (profiles/pmc_traffic.json, written by profiles/summarize.py): HBM bytes
@@ -182,7 +256,7 @@ def load_pmc(workload):
     return {}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -199,23 +273,191 @@ def main():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0 = the job's CPU share: OMP_NUM_THREADS, else the affinity mask)")
-    ap.add_argument("--cpu-row-step", type=int, default=8,
-                    help="CPU baseline: time every k-th row of the frame (8 = one eighth)")
+    ap.add_argument("--cpu-row-step", type=int, default=16,
+                    help="CPU baseline: time every k-th row of the frame (16 = one sixteenth)")
     ap.add_argument("--exact-math", action="store_true",
                     help="PTG_FLAG_EXACT_MATH: the exact fp32 sequences (bit for bit the CPU oracle's Mode B)")
     ap.add_argument("--reference-f64", action="store_true",
                     help="PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode, not the metric)")
     ap.add_argument("--t1", choices=["auto", "off"], default="auto",
-                    help="N > 1: time the same frame on rank 0's GPU alone first (t1_ms, efficiency)")
+                    help="N > 1: time the same frame on one GPU first (t1_ms, efficiency)")
+    ap.add_argument("--t1-steps", type=int, default=3, help="N > 1: frames timed for T1 (after one warm-up)")
     ap.add_argument("--quality-rows", type=int, default=4,
                     help="rows checked against the CPU oracle in the cpu_baseline leg (0 = none)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+
+def frame_config(args, world):
+    wl = args.workload if args.workload != "auto" else ("bench" if world == 1 else "c4")
+    wscene, wW, wH, wspp = WORKLOADS[wl]
+    scene = args.scene or wscene
+    nsub = 2  # main.cpp:202
+    W, H = args.width or wW, args.height or wH
+    samps = (args.spp or wspp) // (nsub * nsub)  # main.cpp:206
+    spp = samps * nsub * nsub
+    wl_name = wl if (scene, W, H, spp) == WORKLOADS[wl] else "custom"
+    return wl_name, scene, W, H, samps, nsub, spp
+
+
+def arith_flags(args):
+    return (ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
+
+
+def arith_name(args):
+    return ("reference f64" if args.reference_f64 else
+            "exact (PTG_FLAG_EXACT_MATH)" if args.exact_math else
+            "fast (hardware v_sqrt/v_rsq/v_rcp/v_sin/v_cos)")
+
+
+def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms, n_sph, pmc):
+    """S_bar*(23*N + 100) + 60 FLOP per sample for the linear
+    scan; generalised to the tests actually executed (BVH scenes): 23 FLOP per
+    ray-sphere test, 12 per slab box test, 100 per segment, 60 per sample.
+    `achieved` is one GPU's kernel: its samples x FLOP/sample / its kernel
+    time (HIP events on the launch stream)."""
+    s_bar = seg_total / frame_samples
+    tests_per_sample = sph_total / frame_samples
+    boxes_per_sample = box_total / frame_samples
+    flop_per_sample = 23 * tests_per_sample + 12 * boxes_per_sample + 100 * s_bar + 60
+    achieved = my_samples * flop_per_sample / (kern_ms / 1e3) / 1e12 if kern_ms > 0 else None
+    return s_bar, {
+        "bound": "valu", "achieved": round(achieved, 3) if achieved else None,
+        "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
+        "segments_per_sample": round(s_bar, 4),
+        # SURVEY.md 8(d)'s conservative "tests-only" model: S_bar*N*23
+        # (linear scenes; the BVH kernel's executed sphere tests otherwise)
+        "frac_tests_only": round(my_samples * 23 * tests_per_sample / (kern_ms / 1e3) / 1e12
+                                 / PEAK_FP32_TFLOPS, 4) if kern_ms > 0 else None,
+        "sphere_tests_per_segment": round(tests_per_sample / s_bar, 2) if s_bar else None,
+        "box_tests_per_segment": round(boxes_per_sample / s_bar, 2) if s_bar else None,
+        "scan": "bvh" if n_sph > 64 else "linear",
+        # measured issue-side view (rocprofv3 profile of this workload,
+        # profiles/<tag>_summary.json): wave64 VALU instructions x 2 cycles
+        # over the 1,024 SIMDs' cycles -- the hardware bound the FLOP model
+        # above does not see
+        "valu_issue_pct_profiled": pmc.get("valu_issue_pct"),
+        "profile": pmc.get("tag")}
+
+
+def base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, parallelism):
+    value = W * H * spp * args.steps / elapsed / 1e6
+    return value, {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mray-samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64 (reference-arithmetic mode)" if args.reference_f64 else "f32",
+        "data": "synthetic (procedural scene from the reference's box_scene.hpp; counter-RNG seed 0x5EED0001)",
+        "config": {"workload": f"{scene} {W}x{H} {spp}spp", "baseline_config": wl_name, "scene": scene,
+                   "width": W, "height": H, "spp": spp, "samples_per_subpixel": samps, "num_subpixels": nsub,
+                   "spheres": n_sph, "band_rows": args.band_rows, "chunk_samples": args.chunk or "auto",
+                   "arithmetic": arith_name(args), "parallelism": parallelism},
+    }
+
+
+def run_inprocess(args):
+    """--gpus N > 1 without a launcher: one process, ptg_multi over GPUs
+    0..N-1 (the scene on every device, ONE ncclGather per frame over xGMI,
+    the un-shard on GPU 0; csrc/ptg_multi.cpp).  A step is one frame kept in
+    HBM.  T1 is the same frame through a one-device ptg_multi (render, slab
+    copy, un-shard), timed the same way."""
+    n = args.gpus
+    rehearsal = os.environ.get("PTG_REHEARSAL") == "1"
+    visible = torch.cuda.device_count()
+    if not rehearsal and visible < n:
+        log(f"error: --gpus {n} needs {n} visible GPUs, {visible} visible (PTG_REHEARSAL=1: {n} shards on GPU 0)")
+        sys.exit(2)
+    wl_name, scene, W, H, samps, nsub, spp = frame_config(args, n)
+    if args.reference_f64:
+        log("error: the multi-GPU path renders the fp32 kernel only (--reference-f64 is a 1-GPU parity mode)")
+        sys.exit(2)
+    scn = ptgpu.make_scene(scene, W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    n_sph = len(scn.spheres)
+    flags = arith_flags(args)
+    params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, 0, 1, args.chunk, flags=flags)
+    cparams = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, 0, 1, args.chunk,
+                                flags=flags | ptgpu.FLAG_COUNT_TESTS)
+    mc = ptgpu.MultiContext(scn, cam, list(range(n)), local_shards=n if rehearsal else 0)
+    counters = mc.frame_device(cparams, counters=True)  # S_bar from the kernels' own counters (untimed)
+    seg_total, sph_total, box_total = (int(v) for v in counters[:3])
+    for _ in range(max(0, args.warmup - 1)):
+        mc.frame_device(params)
+    render_ms, frame_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mc.frame_device(params)  # synchronous: every device done, frame un-sharded on GPU 0
+        r, f = mc.frame_timing()
+        render_ms.append(r)
+        frame_ms.append(f)
+    elapsed = time.perf_counter() - t0
+    image_n = mc.image(params) if args.t1 == "auto" else None
+    mc.close()
+    render_ms = np.array(render_ms)  # [steps, n]
+    kern_dev = render_ms.mean(0)  # per device
+
+    t1 = None
+    if args.t1 == "auto":
+        m1 = ptgpu.MultiContext(scn, cam, [0], local_shards=1)
+        m1.frame_device(params)  # warm-up
+        k1 = max(1, args.t1_steps)
+        r1 = []
+        w0 = time.perf_counter()
+        for _ in range(k1):
+            m1.frame_device(params)
+            r1.append(m1.frame_timing()[0][0])
+        t1_wall = (time.perf_counter() - w0) / k1 * 1e3
+        same = bool(np.array_equal(m1.image(params), image_n))
+        m1.close()
+        t1 = {"wall_ms": round(t1_wall, 3), "kernel_ms": round(float(np.mean(r1)), 3), "frames": k1,
+              "image_equals_n_gpu_frame": same}
+
+    frame_samples = W * H * spp
+    pmc = load_pmc(f"{scene} {W}x{H} {spp}spp")
+    my_samples = frame_samples / n  # equal shards: N divides the bands
+    s_bar, roof = roofline(frame_samples, seg_total, sph_total, box_total, my_samples, float(kern_dev.mean()),
+                           n_sph, pmc)
+    par = (f"tile-sharded row bands x{n}, one process (ptg_multi: ncclCommInitAll + ONE ncclGather per frame)"
+           + (f" -- REHEARSAL: {n} shards on one GPU, gathered by device copies" if rehearsal else ""))
+    value, out = base_line(args, n, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, par)
+    out["segments_per_s"] = round(value * 1e6 * s_bar, 1)
+    out["roofline"] = roof
+    out["roofline"]["note"] = "achieved: one GPU's kernel (mean over the N devices' HIP-event render times)"
+    out["cpu_baseline"] = None
+    out["launch"] = "inprocess"
+    out["per_rank"] = {"render_ms": [round(float(x), 3) for x in kern_dev],
+                       "frame_ms_root": round(float(np.mean(frame_ms)), 3),
+                       "note": "HIP events: each device's render; frame_ms_root = GPU 0's render start to the "
+                               "end of the gather + un-shard"}
+    if t1 is not None:
+        tn_wall = elapsed / args.steps * 1e3
+        tn_kern = float(render_ms.max(1).mean())  # the slowest shard per frame
+        out["t1_ms"] = t1["wall_ms"]
+        out["t1"] = dict(t1, note="the same frame on GPU 0 alone through a one-device ptg_multi, wall clock per "
+                                  "frame like ms_per_step")
+        out["efficiency"] = round(t1["wall_ms"] / (n * tn_wall), 4)
+        out["efficiency_kernel"] = round(t1["kernel_ms"] / (n * tn_kern), 4)
+    print(json.dumps(out), flush=True)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    try:
+        mode, world, rank, local = resolve_launch(args.gpus, os.environ)
+    except ValueError as e:
+        log(f"error: {e}")
+        sys.exit(2)
+    if mode == "inprocess":
+        return run_inprocess(args)
     # PTG_REHEARSAL=1: N ranks on one GPU with gloo (single-GPU box rehearsal
     # of the sharded path); the real multi-GPU run uses nccl (RCCL over xGMI)
     rehearsal = os.environ.get("PTG_REHEARSAL") == "1"
@@ -229,17 +471,11 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    wl = args.workload if args.workload != "auto" else ("bench" if world == 1 else "c4")
-    wscene, wW, wH, wspp = WORKLOADS[wl]
-    args.scene = args.scene or wscene
-    nsub = 2  # main.cpp:202
-    W, H = args.width or wW, args.height or wH
-    samps = (args.spp or wspp) // (nsub * nsub)  # main.cpp:206
-    spp = samps * nsub * nsub
-    scn = ptgpu.make_scene(args.scene, W, H)
+    wl_name, scene, W, H, samps, nsub, spp = frame_config(args, world)
+    scn = ptgpu.make_scene(scene, W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     ctx = ptgpu.Context(scn, cam, device=local)
-    f64 = (ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
+    f64 = arith_flags(args)
     params = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
                                flags=f64)
     cparams = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, rank, world, args.chunk,
@@ -274,23 +510,29 @@ def main():
     torch.cuda.synchronize()
 
     # N > 1: the same frame rendered by rank 0 alone (shard_count 1), untimed
-    # with respect to `value` -- the driver's 1-GPU BENCH line is the 1080p
-    # frame, so the N-GPU line carries its own same-frame T1 and efficiency
+    # with respect to `value`, timed like a step: wall clock per frame of
+    # render + un-shard (the one-slab "gather" is the identity), plus its
+    # kernel's HIP events
     t1_frame = None
     if world > 1 and args.t1 == "auto":
         if rank == 0:
             p1 = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, 0, 1, args.chunk, flags=f64)
             full = torch.empty(ptgpu.shard_rows(H, args.band_rows, 1) * W * 3, dtype=torch.float32, device=dev)
+            img1 = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
             ctx.render_device(full, p1, None, stream)  # warm-up (allocates the accumulator)
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            k1 = max(1, args.t1_steps)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k1)]
             w0 = time.perf_counter()
-            e0.record(stream)
-            ctx.render_device(full, p1, None, stream)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            t1_frame = {"ms": round(e0.elapsed_time(e1), 3), "wall_ms": round((time.perf_counter() - w0) * 1e3, 3)}
-            del full
+            for e0, e1 in ev:
+                e0.record(stream)
+                ctx.render_device(full, p1, None, stream)
+                e1.record(stream)
+                ptgpu.unshard_device(full, img1, W, H, args.band_rows, 1, stream)
+                torch.cuda.synchronize()
+            t1_frame = {"wall_ms": round((time.perf_counter() - w0) / k1 * 1e3, 3),
+                        "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 3), "frames": k1}
+            del full, img1
         dist.barrier()
 
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
@@ -308,6 +550,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs])) if args.steps else float("nan")
     gather_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs])) if args.steps else float("nan")
     per_rank = None
+    kern_max = kern_ms
     if world > 1:  # per-rank render and gather (+ un-shard on rank 0) times, HIP events on the launch stream
         cdev0 = torch.device("cpu") if rehearsal else dev
         mine = torch.tensor([kern_ms, gather_ms], dtype=torch.float64, device=cdev0)
@@ -316,91 +559,44 @@ def main():
         per_rank = {"render_ms": [round(float(t[0]), 3) for t in allr],
                     "gather_ms": [round(float(t[1]), 3) for t in allr],
                     "note": "gather_ms: the RCCL gather (and rank 0's un-shard), incl. waiting for the slowest rank"}
+        kern_max = max(float(t[0]) for t in allr)
 
     seg_total = seg_local
     if world > 1:
         cdev = torch.device("cpu") if rehearsal else dev
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=cdev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
         s = torch.tensor([seg_local, sph_local, box_local], dtype=torch.int64, device=cdev)
         dist.all_reduce(s)
         seg_total, sph_local, box_local = (int(v) for v in s.cpu().tolist())
-    frame_samples = W * H * spp
-    s_bar = seg_total / frame_samples
-    n_sph = ctx.n_spheres
-    # S_bar*(23*N + 100) + 60 per sample for the linear scan;
-    # generalised to the tests actually executed (BVH scenes): 23 FLOP per
-    # ray-sphere test, 12 per slab box test, 100 per segment, 60 per sample
-    tests_per_sample = sph_local / frame_samples
-    boxes_per_sample = box_local / frame_samples
-    flop_per_sample = 23 * tests_per_sample + 12 * boxes_per_sample + 100 * s_bar + 60
-    my_samples = my_rows * W * spp
-    achieved = my_samples * flop_per_sample / (kern_ms / 1e3) / 1e12 if kern_ms > 0 else None
 
     if rank == 0:
-        workload = f"{args.scene} {W}x{H} {spp}spp"
-        wl_name = wl if (args.scene, W, H, spp) == WORKLOADS[wl] else "custom"
-        value = frame_samples * args.steps / elapsed / 1e6
+        frame_samples = W * H * spp
+        pmc = load_pmc(f"{scene} {W}x{H} {spp}spp")
+        s_bar, roof = roofline(frame_samples, seg_total, sph_local, box_local, my_rows * W * spp, kern_ms,
+                               ctx.n_spheres, pmc)
+        par = ((f"tile-sharded row bands x{world}, one process per GPU (torch.distributed nccl = RCCL)"
+                + (" (gloo rehearsal on one GPU)" if rehearsal else "")) if world > 1 else "single GPU")
+        value, out = base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, ctx.n_spheres, elapsed, par)
+        out["segments_per_s"] = round(value * 1e6 * s_bar, 1)
+        out["roofline"] = roof
         cpu = None
         if world == 1 and args.cpu_baseline == "auto":
             frame = slab.cpu().numpy().reshape(rows, W, 3)[:H]  # band_rows = 1, one shard: slab row = image row
-            cpu = cpu_baseline(args.scene, W, H, samps, nsub, args.cpu_threads or default_cpu_threads(),
+            cpu = cpu_baseline(scene, W, H, samps, nsub, args.cpu_threads or default_cpu_threads(),
                                max(1, args.cpu_row_step), frame, ptgpu.DEFAULT_SEED, args.quality_rows)
-        pmc = load_pmc(workload)
-        traffic = pmc.get("hbm_bytes_per_launch")
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "Mray-samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "segments_per_s": round(value * 1e6 * s_bar, 1),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f64 (reference-arithmetic mode)" if args.reference_f64 else "f32",
-            "data": "synthetic (procedural scene from the reference's box_scene.hpp; counter-RNG seed 0x5EED0001)",
-            "config": {"workload": workload, "baseline_config": wl_name, "scene": args.scene, "width": W, "height": H, "spp": spp,
-                       "samples_per_subpixel": samps, "num_subpixels": nsub, "spheres": n_sph,
-                       "band_rows": args.band_rows, "chunk_samples": args.chunk or "auto",
-                       "arithmetic": ("reference f64" if args.reference_f64 else
-                                      "exact (PTG_FLAG_EXACT_MATH)" if args.exact_math else
-                                      "fast (hardware v_sqrt/v_rsq/v_rcp/v_sin/v_cos)"),
-                       "parallelism": (f"tile-sharded row bands x{world}" + (" (gloo rehearsal on one GPU)"
-                                                                              if rehearsal else ""))
-                       if world > 1 else "single GPU"},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3) if achieved else None,
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
-                         "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
-                         "segments_per_sample": round(s_bar, 4),
-                         # SURVEY.md 8(d)'s conservative "tests-only" model: S_bar*N*23
-                         # (linear scenes; the BVH kernel's executed sphere tests otherwise)
-                         "frac_tests_only": round(my_samples * 23 * tests_per_sample / (kern_ms / 1e3) / 1e12
-                                                  / PEAK_FP32_TFLOPS, 4) if kern_ms > 0 else None,
-                         "sphere_tests_per_segment": round(tests_per_sample / s_bar, 2) if s_bar else None,
-                         "box_tests_per_segment": round(boxes_per_sample / s_bar, 2) if s_bar else None,
-                         "scan": "bvh" if n_sph > 64 else "linear",
-                         # measured issue-side view (rocprofv3 profile of this workload,
-                         # profiles/<tag>_summary.json): wave64 VALU instructions x 2 cycles
-                         # over the 1,024 SIMDs' cycles -- the hardware bound the FLOP model
-                         # above does not see
-                         "valu_issue_pct_profiled": pmc.get("valu_issue_pct"),
-                         "profile": pmc.get("tag")},
-            "cpu_baseline": cpu,
-        }
+        out["cpu_baseline"] = cpu
+        out["launch"] = "torchrun" if world > 1 else "single"
         if per_rank is not None:
             out["per_rank"] = per_rank
         if t1_frame is not None:
-            # efficiency of this run = T1 / (N * T_N), both on this node in this run
-            out["t1_ms"] = t1_frame["ms"]
-            out["t1"] = dict(t1_frame, note="the same frame on rank 0's GPU alone (HIP events; no gather), "
-                                            "untimed for value")
-            out["efficiency"] = round(t1_frame["ms"] / (world * elapsed / args.steps * 1e3), 4)
+            tn_wall = elapsed / args.steps * 1e3
+            out["t1_ms"] = t1_frame["wall_ms"]
+            out["t1"] = dict(t1_frame, note="the same frame on rank 0's GPU alone (render + un-shard), wall clock "
+                                            "per frame like ms_per_step; kernel_ms from HIP events")
+            out["efficiency"] = round(t1_frame["wall_ms"] / (world * tn_wall), 4)
+            out["efficiency_kernel"] = round(t1_frame["kernel_ms"] / (world * kern_max), 4)
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)

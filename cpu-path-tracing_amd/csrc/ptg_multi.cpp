@@ -38,8 +38,10 @@ struct Shard {
     ptg_context *ctx = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // local transport: the slab is complete
+    hipEvent_t t_begin = nullptr, t_rendered = nullptr;  // timing of the last device frame
     float *slab = nullptr;
     size_t slab_cap = 0;  // floats
+    unsigned long long *counters = nullptr;  // PTG_FLAG_COUNT_TESTS: 4 per shard
     ncclComm_t comm = nullptr;
 };
 
@@ -81,6 +83,12 @@ struct ptg_multi {
     float *image = nullptr;  // root: the un-sharded frame
     size_t image_cap = 0;
     std::vector<float> host;
+    hipEvent_t t_unsharded = nullptr;  // root: the frame is un-sharded
+    bool timed = false;  // the events hold a completed ptg_multi_frame_device
+    // a failure inside the RCCL group: the communicators were aborted and the
+    // context refuses further frames (PTG_ERR_HIP) until destroyed
+    bool broken = false;
+    int inject_gather_fault = -1;  // tests: fail ncclGather at this shard
 };
 
 namespace {
@@ -91,7 +99,7 @@ int destroy(ptg_multi *m)
         return PTG_OK;
     DeviceGuard g;
     for (Shard &s : m->shards) {
-        if (s.id < 0)
+        if (s.id < 0 || m->broken)  // a broken group's streams are not waited on
             continue;
         (void)hipSetDevice(s.id);
         if (s.stream)
@@ -102,11 +110,17 @@ int destroy(ptg_multi *m)
             continue;
         (void)hipSetDevice(s.id);
         if (s.comm)
-            (void)ncclCommDestroy(s.comm);
+            (void)(m->broken ? ncclCommAbort(s.comm) : ncclCommDestroy(s.comm));
         if (s.slab)
             (void)hipFree(s.slab);
+        if (s.counters)
+            (void)hipFree(s.counters);
         if (s.done)
             (void)hipEventDestroy(s.done);
+        if (s.t_begin)
+            (void)hipEventDestroy(s.t_begin);
+        if (s.t_rendered)
+            (void)hipEventDestroy(s.t_rendered);
         if (s.stream)
             (void)hipStreamDestroy(s.stream);
         if (s.ctx)
@@ -118,6 +132,8 @@ int destroy(ptg_multi *m)
             (void)hipFree(m->gathered);
         if (m->image)
             (void)hipFree(m->image);
+        if (m->t_unsharded)
+            (void)hipEventDestroy(m->t_unsharded);
     }
     delete m;
     return PTG_OK;
@@ -156,6 +172,12 @@ int create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, c
             e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
         if (e == hipSuccess)
             e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        if (e == hipSuccess)
+            e = hipEventCreate(&s.t_begin);
+        if (e == hipSuccess)
+            e = hipEventCreate(&s.t_rendered);
+        if (e == hipSuccess && k == 0)
+            e = hipEventCreate(&m->t_unsharded);
         if (e != hipSuccess)
             rc = hip_fail("multi: stream/event", e);
     }
@@ -180,6 +202,9 @@ int check_frame(const ptg_multi *m, const ptg_params *p)
 {
     if (!m || !p)
         return fail(PTG_ERR_INVALID_ARGUMENT, "multi: NULL context or params");
+    if (m->broken)
+        return fail(PTG_ERR_HIP, "multi: the context's RCCL group failed earlier and its communicators were "
+                                 "aborted; destroy it");
     if (p->width <= 0 || p->height <= 0 || p->band_rows < 1)
         return fail(PTG_ERR_INVALID_ARGUMENT, "multi: width, height and band_rows must be positive");
     if (p->shard_count != 1 || p->shard_rank != 0)
@@ -251,35 +276,46 @@ int reserve(ptg_multi *m, const ptg_params *p, size_t &slab_elems)
 
 // ONE gather of the equal-size slabs to the root (RCCL: one ncclGather per
 // rank inside a group, rank-major on the root -- rccl.h:745; local shards: the
-// same layout by device copies after each shard's slab is complete), the
-// un-shard there, and the image to the host (m->host).  Synchronous.
-int gather_unshard(ptg_multi *m, const ptg_params *p, size_t slab_elems)
+// same layout by device copies after each shard's slab is complete) and the
+// un-shard there, queued on the root's stream (asynchronous).
+int gather_unshard_device(ptg_multi *m, const ptg_params *p, size_t slab_elems)
 {
     const int n = (int)m->shards.size();
     Shard &root = m->shards[0];
     if (m->rccl) {
+        // every device is made current once BEFORE the group opens, so that
+        // inside it only the ncclGather calls can fail
+        for (int k = n - 1; k >= 0; --k)
+            MULTI_HIP(hipSetDevice(m->shards[k].id));
         ncclResult_t r = ncclGroupStart();
         if (r != ncclSuccess)
             return nccl_fail("ncclGroupStart", r);
         int rc = PTG_OK;
         for (int k = 0; k < n && rc == PTG_OK; ++k) {
             Shard &s = m->shards[k];
-            hipError_t e = hipSetDevice(s.id);
-            if (e != hipSuccess) {
-                rc = hip_fail("hipSetDevice", e);
-                break;
-            }
-            r = ncclGather(s.slab, k == 0 ? m->gathered : nullptr, slab_elems, ncclFloat, 0, s.comm, s.stream);
+            (void)hipSetDevice(s.id);
+            r = k == m->inject_gather_fault
+                    ? ncclInvalidArgument
+                    : ncclGather(s.slab, k == 0 ? m->gathered : nullptr, slab_elems, ncclFloat, 0, s.comm, s.stream);
             if (r != ncclSuccess)
                 rc = nccl_fail("ncclGather", r);
         }
         // the group is closed on every path (an error inside it must not leave
-        // this thread's RCCL group open)
-        r = ncclGroupEnd();
-        if (rc != PTG_OK)
-            return rc;
-        if (r != ncclSuccess)
-            return nccl_fail("ncclGroupEnd", r);
+        // this thread's RCCL group open) ...
+        const ncclResult_t re = ncclGroupEnd();
+        if (rc != PTG_OK || re != ncclSuccess) {
+            // ... but a partial group must not run without its peers: the
+            // queued collectives are aborted with the communicators, and the
+            // context refuses further frames
+            m->broken = true;
+            for (Shard &s : m->shards)
+                if (s.comm) {
+                    (void)hipSetDevice(s.id);
+                    (void)ncclCommAbort(s.comm);
+                    s.comm = nullptr;
+                }
+            return rc != PTG_OK ? rc : nccl_fail("ncclGroupEnd", re);
+        }
         MULTI_HIP(hipSetDevice(root.id));
     } else {
         MULTI_HIP(hipSetDevice(root.id));
@@ -291,19 +327,31 @@ int gather_unshard(ptg_multi *m, const ptg_params *p, size_t slab_elems)
                                      hipMemcpyDeviceToDevice, root.stream));
         }
     }
-    int rc = ptg_unshard_device(m->gathered, m->image, p->width, p->height, p->band_rows, n, root.stream);
-    if (rc)
-        return rc;
-    const size_t image_elems = (size_t)p->width * p->height * 3;
-    MULTI_HIP(hipMemcpyAsync(m->host.data(), m->image, image_elems * sizeof(float), hipMemcpyDeviceToHost,
-                             root.stream));
-    MULTI_HIP(hipStreamSynchronize(root.stream));
-    // the other shards' streams: their part ended with the gather
-    for (int k = 1; k < n; ++k) {
+    return ptg_unshard_device(m->gathered, m->image, p->width, p->height, p->band_rows, n, root.stream);
+}
+
+// waits for every shard's stream (root last: its part ends with the un-shard)
+int sync_all(ptg_multi *m)
+{
+    for (int k = (int)m->shards.size() - 1; k >= 0; --k) {
         MULTI_HIP(hipSetDevice(m->shards[k].id));
         MULTI_HIP(hipStreamSynchronize(m->shards[k].stream));
     }
     return PTG_OK;
+}
+
+// gather + un-shard, then the image to the host (m->host).  Synchronous.
+int gather_unshard(ptg_multi *m, const ptg_params *p, size_t slab_elems)
+{
+    int rc = gather_unshard_device(m, p, slab_elems);
+    if (rc)
+        return rc;
+    Shard &root = m->shards[0];
+    const size_t image_elems = (size_t)p->width * p->height * 3;
+    MULTI_HIP(hipSetDevice(root.id));
+    MULTI_HIP(hipMemcpyAsync(m->host.data(), m->image, image_elems * sizeof(float), hipMemcpyDeviceToHost,
+                             root.stream));
+    return sync_all(m);
 }
 
 }  // namespace
@@ -408,6 +456,94 @@ int ptg_multi_resolve(ptg_multi *m, const ptg_params *params, int32_t samples_do
         return rc;
     const size_t image_elems = (size_t)params->width * params->height * 3;
     std::copy(m->host.begin(), m->host.begin() + image_elems, image_rgb);
+    return PTG_OK;
+}
+
+int ptg_multi_frame_device(ptg_multi *m, const ptg_params *params, unsigned long long *counters)
+{
+    int rc = check_frame(m, params);
+    if (rc)
+        return rc;
+    DeviceGuard g;
+    size_t slab_elems = 0;
+    if ((rc = reserve(m, params, slab_elems)))
+        return rc;
+    const int n = (int)m->shards.size();
+    const bool count = (params->flags & (PTG_FLAG_COUNT_TESTS | PTG_FLAG_COUNT_NONFINITE)) != 0;
+    m->timed = false;
+    for (int k = 0; k < n; ++k) {
+        Shard &s = m->shards[k];
+        MULTI_HIP(hipSetDevice(s.id));
+        if (count && !s.counters && hipMalloc(&s.counters, 4 * sizeof(unsigned long long)) != hipSuccess)
+            return fail(PTG_ERR_OUT_OF_MEMORY, "multi: hipMalloc of the counters failed");
+        if (count)
+            MULTI_HIP(hipMemsetAsync(s.counters, 0, 4 * sizeof(unsigned long long), s.stream));
+        MULTI_HIP(hipEventRecord(s.t_begin, s.stream));
+        const ptg_params q = shard_params(params, k, n);
+        if ((rc = ptg_render_device(s.ctx, &q, s.slab, count ? s.counters : nullptr, s.stream)))
+            return rc;
+        MULTI_HIP(hipSetDevice(s.id));
+        MULTI_HIP(hipEventRecord(s.t_rendered, s.stream));
+    }
+    if ((rc = gather_unshard_device(m, params, slab_elems)))
+        return rc;
+    MULTI_HIP(hipSetDevice(m->shards[0].id));
+    MULTI_HIP(hipEventRecord(m->t_unsharded, m->shards[0].stream));
+    if ((rc = sync_all(m)))
+        return rc;
+    m->timed = true;
+    if (count && counters) {
+        for (int i = 0; i < 4; ++i)
+            counters[i] = 0;
+        for (Shard &s : m->shards) {
+            unsigned long long c[4];
+            MULTI_HIP(hipSetDevice(s.id));
+            MULTI_HIP(hipMemcpy(c, s.counters, sizeof(c), hipMemcpyDeviceToHost));
+            for (int i = 0; i < 4; ++i)
+                counters[i] += c[i];
+        }
+    }
+    return PTG_OK;
+}
+
+int ptg_multi_frame_timing(const ptg_multi *m, float *render_ms, int n, float *frame_ms)
+{
+    if (!m || !m->timed)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_frame_timing: no completed ptg_multi_frame_device");
+    if (n != (int)m->shards.size() || !render_ms || !frame_ms)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_frame_timing: render_ms needs one entry per device");
+    DeviceGuard g;
+    for (int k = 0; k < n; ++k) {
+        MULTI_HIP(hipSetDevice(m->shards[k].id));
+        MULTI_HIP(hipEventElapsedTime(&render_ms[k], m->shards[k].t_begin, m->shards[k].t_rendered));
+    }
+    MULTI_HIP(hipSetDevice(m->shards[0].id));
+    MULTI_HIP(hipEventElapsedTime(frame_ms, m->shards[0].t_begin, m->t_unsharded));
+    return PTG_OK;
+}
+
+int ptg_multi_image(ptg_multi *m, const ptg_params *params, float *image_rgb)
+{
+    int rc = check_frame(m, params);
+    if (rc)
+        return rc;
+    if (!image_rgb || !m->timed)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_image: NULL image or no completed ptg_multi_frame_device");
+    const size_t image_elems = (size_t)params->width * params->height * 3;
+    if (image_elems > m->image_cap)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_image: params larger than the last frame");
+    DeviceGuard g;
+    MULTI_HIP(hipSetDevice(m->shards[0].id));
+    MULTI_HIP(hipMemcpy(image_rgb, m->image, image_elems * sizeof(float), hipMemcpyDeviceToHost));
+    return PTG_OK;
+}
+
+// internal (tests): make the next RCCL gather fail at shard k (-1: off)
+int ptg_multi_inject_gather_fault_(ptg_multi *m, int k)
+{
+    if (!m)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi: NULL context");
+    m->inject_gather_fault = k;
     return PTG_OK;
 }
 

@@ -11,7 +11,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # PTGPU_LIB selects an alternative build of the same ABI (A/B experiments only)
 LIB_PATH = os.environ.get("PTGPU_LIB") or os.path.join(PKG_DIR, "libptgpu.so")
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/ptgpu.h PTG_ABI_VERSION
 
 # every symbol include/ptgpu.h declares
 EXPORTS = (
@@ -20,7 +20,8 @@ EXPORTS = (
     "ptg_unshard_device", "ptg_tonemap_device", "ptg_trace_samples_device",
     "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device", "ptg_scene_layout",
     "ptg_render_multi", "ptg_multi_create", "ptg_multi_destroy", "ptg_multi_render",
-    "ptg_multi_reset_accumulation", "ptg_multi_accumulate", "ptg_multi_resolve", "ptg_math_probe_device",
+    "ptg_multi_reset_accumulation", "ptg_multi_accumulate", "ptg_multi_resolve", "ptg_multi_frame_device",
+    "ptg_multi_frame_timing", "ptg_multi_image", "ptg_math_probe_device",
 )
 
 
@@ -73,6 +74,10 @@ def lib():
             "ptg_multi_reset_accumulation": (I, [P, C.POINTER(Params)]),
             "ptg_multi_accumulate": (I, [P, C.POINTER(Params), C.c_int32, C.c_int32]),
             "ptg_multi_resolve": (I, [P, C.POINTER(Params), C.c_int32, P]),
+            "ptg_multi_frame_device": (I, [P, C.POINTER(Params), P]),
+            "ptg_multi_frame_timing": (I, [P, P, I, P]),
+            "ptg_multi_image": (I, [P, C.POINTER(Params), P]),
+            "ptg_multi_inject_gather_fault_": (I, [P, I]),
             # internal (tests): n shards on one device, gathered by device copies
             "ptg_multi_create_local_": (I, [P, C.c_size_t, P, I, I, C.POINTER(C.c_void_p)]),
         }

@@ -140,6 +140,7 @@ class MultiContext:
             check(lib().ptg_multi_create(sp.ctypes.data_as(C.c_void_p), len(sp), ca.ctypes.data_as(C.c_void_p), devs,
                                          len(devices), C.byref(h)), "ptg_multi_create")
         self._h = h
+        self.n_devices = int(local_shards) if local_shards else len(devices)
 
     def close(self):
         if self._h:
@@ -170,6 +171,33 @@ class MultiContext:
         check(lib().ptg_multi_render(self._h, C.byref(params), self._image(image, params, np.float64)),
               "ptg_multi_render")
         return image
+
+    def frame_device(self, params: Params, counters: bool = False):
+        """ptg_multi_frame_device: the frame over all devices, kept in HBM
+        (render, ONE gather, un-shard; synchronous).  With counters=True
+        (params needs FLAG_COUNT_TESTS) returns the 4 summed kernel counters."""
+        c = np.zeros(4, dtype=np.uint64)
+        check(lib().ptg_multi_frame_device(self._h, C.byref(params), c.ctypes.data_as(C.c_void_p) if counters else None),
+              "ptg_multi_frame_device")
+        return c if counters else None
+
+    def frame_timing(self):
+        """(render_ms per device, frame_ms on the root) of the last frame_device."""
+        r = np.zeros(self.n_devices, dtype=np.float32)
+        f = np.zeros(1, dtype=np.float32)
+        check(lib().ptg_multi_frame_timing(self._h, r.ctypes.data_as(C.c_void_p), self.n_devices,
+                                           f.ctypes.data_as(C.c_void_p)), "ptg_multi_frame_timing")
+        return r.astype(float).tolist(), float(f[0])
+
+    def image(self, params: Params) -> np.ndarray:
+        """The last frame_device image, [H, W, 3] float32 in the reference's row order."""
+        out = np.empty(params.width * params.height * 3, dtype=np.float32)
+        check(lib().ptg_multi_image(self._h, C.byref(params), out.ctypes.data_as(C.c_void_p)), "ptg_multi_image")
+        return out.reshape(params.height, params.width, 3)
+
+    def inject_gather_fault_(self, shard: int) -> None:
+        """Tests: the next RCCL gather fails at `shard` (-1: off)."""
+        check(lib().ptg_multi_inject_gather_fault_(self._h, int(shard)), "ptg_multi_inject_gather_fault_")
 
     def reset_accumulation(self, params: Params) -> None:
         check(lib().ptg_multi_reset_accumulation(self._h, C.byref(params)), "ptg_multi_reset_accumulation")

@@ -24,7 +24,12 @@
 extern "C" {
 #endif
 
-#define PTG_ABI_VERSION 1
+/* 2: flags = 0 now selects the fast arithmetic mode (hardware
+ * transcendentals, not reproducible on a CPU); version 1's flags = 0 was the
+ * oracle-exact mode, now PTG_FLAG_EXACT_MATH.  Also added since 1:
+ * ptg_multi_*, ptg_math_probe_device.  A caller built against 1 that needs
+ * the old bit-exact image must pass PTG_FLAG_EXACT_MATH. */
+#define PTG_ABI_VERSION 2
 
 typedef enum ptg_status {
     PTG_OK = 0,
@@ -103,7 +108,7 @@ typedef struct ptg_params {
  * doubles; ptg_render_device rounds them into its float slab.  Not for
  * progressive passes or trace_samples (PTG_ERR_UNSUPPORTED). */
 #define PTG_FLAG_REFERENCE_F64 4
-/* PTG_FLAG_EXACT_MATH: the fp32 kernel with deterministic square root,
+/* PTG_FLAG_EXACT_MATH (ABI 2; the default of ABI 1): the fp32 kernel with deterministic square root,
  * reciprocal square root, division and sin/cos sequences (~1 ulp) that the
  * oracle (oracle/pt_oracle.c, Mode B) executes too -- the image then equals
  * the CPU restatement bit for bit.  Without it (the default) the kernel uses
@@ -165,6 +170,21 @@ int ptg_multi_render(ptg_multi *m, const ptg_params *params, double *image_rgb);
 int ptg_multi_reset_accumulation(ptg_multi *m, const ptg_params *params);
 int ptg_multi_accumulate(ptg_multi *m, const ptg_params *params, int32_t sample_begin, int32_t sample_end);
 int ptg_multi_resolve(ptg_multi *m, const ptg_params *params, int32_t samples_done, float *image_rgb);
+/* The frame kept in HBM (the benchmark step over several GPUs): every device
+ * renders its bands, ONE gather, the un-shard into the root's image buffer;
+ * returns when all devices are done, with no host copy of the image.  With
+ * PTG_FLAG_COUNT_TESTS in params->flags, counters (optional, host, 4 values)
+ * receives the counters of ptg_render_device summed over the devices.
+ * ptg_multi_frame_timing then gives, from HIP events of that frame, each
+ * device's render time (render_ms[n_devices]) and the root's time from the
+ * start of its render to the end of the un-shard (frame_ms);
+ * ptg_multi_image copies the frame (W*H*3 floats, reference row order) to the
+ * host.  After a failure inside the RCCL group the communicators are aborted
+ * (no partial collective runs) and every later frame call returns
+ * PTG_ERR_HIP; destroy the context. */
+int ptg_multi_frame_device(ptg_multi *m, const ptg_params *params, unsigned long long *counters);
+int ptg_multi_frame_timing(const ptg_multi *m, float *render_ms, int n_devices, float *frame_ms);
+int ptg_multi_image(ptg_multi *m, const ptg_params *params, float *image_rgb);
 
 /* ---- device-resident path (bench, multi-GPU) --------------------------
  * A context holds the prepared scene in HBM on one device. */

@@ -126,3 +126,55 @@ def test_partial_pixel_group_with_the_largest_chunk():
     gpu = out.cpu().numpy().reshape(H, W, 3)
     b, _ = po.render_xs_rect(sp, ca, W, H, samps, nsub, SEED, nthreads=16)
     assert np.array_equal(gpu, b)
+
+
+@pytest.mark.parametrize("local", [0, 2, 8])
+def test_multi_frame_device_equals_one_gpu_frame(local):
+    """ptg_multi_frame_device (bench.py's N-GPU step, kept in HBM): the
+    un-sharded frame equals the 1-device frame bit for bit, the summed
+    counters equal the 1-device counters, and the frame's HIP-event timings
+    are positive."""
+    _require_gpu()
+    W, H, samps = 64, 40, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    p = ptgpu.make_params(W, H, samps, 2, SEED, 1, flags=ptgpu.FLAG_COUNT_TESTS)
+    ref = np.zeros((H * W, 3))
+    ptgpu.render(scn, cam, ref, W, H, samps)
+    with ptgpu.Context(scn, cam) as ctx:
+        slab = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
+        segs = torch.zeros(3, dtype=torch.int64, device="cuda")
+        ctx.render_device(slab, p, segs)
+        torch.cuda.synchronize()
+        ref_counts = segs.cpu().tolist()
+    with ptgpu.MultiContext(scn, cam, [0], local_shards=local) as m:
+        for _ in range(2):  # the context is reused
+            c = m.frame_device(p, counters=True)
+            img = m.image(p)
+            assert np.array_equal(img.reshape(-1, 3).astype(np.float64), ref)
+            assert [int(v) for v in c[:3]] == ref_counts
+            r, f = m.frame_timing()
+            assert len(r) == m.n_devices and min(r) > 0 and f >= max(r) * 0.5
+
+
+def test_multi_gather_fault_aborts_the_group():
+    """a failure inside the RCCL group does not launch a partial
+    gather -- the communicators are aborted, the frame reports the error,
+    later frames are refused, and destroying the context does not hang."""
+    _require_gpu()
+    W, H, samps = 32, 16, 2
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    p = ptgpu.make_params(W, H, samps, 2, SEED, 1)
+    m = ptgpu.MultiContext(scn, cam, [0])
+    m.frame_device(p)  # a good frame first
+    m.inject_gather_fault_(0)
+    with pytest.raises(ptgpu.PtgError, match="ncclGather"):
+        m.frame_device(p)
+    with pytest.raises(ptgpu.PtgError, match="aborted"):
+        m.frame_device(p)
+    m.close()
+    # the device is still usable
+    img = np.zeros((H * W, 3))
+    ptgpu.render(scn, cam, img, W, H, samps)
+    assert img.mean() > 0
