@@ -180,15 +180,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_LDS_ROOT
 #define PTG_BVH_LDS_ROOT 0  // A/B: the root wide node of every octant layout read from LDS
 #endif
-#ifndef PTG_BVH_POS_WINNER
-// BVH scenes: the scan's winner is kept as a POSITION (leaf order, then the
-// huge spheres), with the shading records stored in that order; the scene
-// index -- needed only to break an exact tie of t (main.cpp:35's lowest
-// index) -- is loaded only on such a tie.  Before, every improving candidate
-// loaded its scene index in the leaf loop (a dependent global load and wait
-// per win).  Same winner, same bits.
-#define PTG_BVH_POS_WINNER 1
-#endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
                           // (measured with octant layouts + SAH: 6 beats 4 by 7 %, 5 and 7 by 1-2 %)
@@ -282,8 +273,6 @@ struct KArgs {
     float q_lo[3], q_scale[3];  // box grid: plane = q_lo + value * q_scale (binary: u16 values; wide: binary16)
     const float4 *bvh_sph;    // leaf-ordered spheres {C, -R^2} (BVH leaves hold only non-huge spheres)
     const int *bvh_id;        // leaf-ordered scene indices
-    const int *pos_id;        // PTG_BVH_POS_WINNER: scene index of every position (leaves, then huge spheres)
-    int n_leaf;               // positions of the huge spheres start here
     const GeoRec *big_geo;    // huge spheres, tested linearly
     const int *big_id;
     int n_nodes, n_big;
@@ -763,30 +752,13 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
 // lowest scene index (main.cpp:35: strict < in index order), which makes the
 // result independent of the visiting order: the oracle's linear scan
 // (intersect_B_lex) gives the same bits.
-[[maybe_unused]] __device__ __forceinline__ void update_lex(const float t, const int sid, float &tb, int &best)
+__device__ __forceinline__ void update_lex(const float t, const int sid, float &tb, int &best)
 {
     // a NaN t (rejected) fails both compares; (unsigned) -1 orders after every
     // index.  Selects, not a short-circuit && / || (exec-masked blocks)
     const bool win = (t < tb) | ((t == tb) & ((unsigned)sid < (unsigned)best));
     tb = win ? t : tb;
     best = win ? sid : best;
-}
-
-// The same rule on positions (PTG_BVH_POS_WINNER): candidate pos against the
-// current best position; the scene indices are read only for an exact tie
-// of t (never in practice -- the branch keeps the loads out of the common
-// path).  best = -1: none yet (any candidate wins a tie with it).
-__device__ __forceinline__ void update_lex_pos(const float t, const int pos, float &tb, int &best,
-                                               const int *__restrict__ pos_id)
-{
-    bool win = t < tb;
-    if (t == tb) {  // exec-masked: entered by tying lanes only
-        // pos = -1: no candidate (a helper that found nothing reports the
-        // owner's tb back, a tie by construction) -- never wins
-        win = pos >= 0 && (best < 0 || (unsigned)pos_id[pos] < (unsigned)pos_id[best]);
-    }
-    tb = win ? t : tb;
-    best = win ? pos : best;
 }
 
 // Per-lane BVH scan state.  The render kernel keeps it across iterations of
@@ -858,12 +830,7 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.tb = kInf;
     tr.best = -1;
     for (int k = 0; k < A.n_big; ++k)
-#if PTG_BVH_POS_WINNER
-        update_lex_pos(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.n_leaf + k, tr.tb,
-                       tr.best, A.pos_id);
-#else
         update_lex(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
-#endif
     if constexpr (kCount)
         cnt.spheres += A.n_big;
 #if PTG_BVH_WIDE
@@ -1098,12 +1065,8 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
         sc.spheres += cnt;
     for (int j = 0; j < cnt; ++j) {
         const float t = root_lex<false, kExact>(A.bvh_sph[f + j], float4{}, o, d, a, tb);
-#if PTG_BVH_POS_WINNER
-        update_lex_pos(t, f + j, tb, best, A.pos_id);
-#else
         if (t <= tb)  // the scene index is read only for a candidate that wins or ties
             update_lex(t, A.bvh_id[f + j], tb, best);
-#endif
     }
 }
 
@@ -1225,13 +1188,8 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     const float htb = bpf(partner, tb), htb2 = bpf(partner2, tb);
     const int hbest = bpi(partner, best), hbest2 = bpi(partner2, best);
     if (po) {
-#if PTG_BVH_POS_WINNER
-        update_lex_pos(htb, hbest, tb, best, A.pos_id);
-        update_lex_pos(htb2, hbest2, tb, best, A.pos_id);  // partner2 = lane without a second helper: a no-op
-#else
         update_lex(htb, hbest, tb, best);
         update_lex(htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
-#endif
     }
 #if PTG_BVH_WIDE && PTG_LEAF_DONE_SEL
     tr.tb = has ? tb : tr.tb;
@@ -2766,8 +2724,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t off_id = off_geo + n_leaf * sizeof(float4);
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
-        const size_t off_pid = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
-        const size_t off_q = (off_pid + (n_leaf + n_big) * sizeof(int) + 15) & ~size_t(15);
+        const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
 #if PTG_BVH_WIDE
         const size_t n_recs = wide_bvh(b, 0, 0).size();  // records per layout
 #else
@@ -2831,25 +2788,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             std::memcpy(blob.data() + off_bgeo + i * sizeof(GeoRec), &geo[b.big[i]], sizeof(GeoRec));
             std::memcpy(blob.data() + off_bid + i * sizeof(int), &b.big[i], sizeof(int));
         }
-        // positions: the leaf order, then the huge spheres (PTG_BVH_POS_WINNER)
-        std::vector<int> pos_scene(n_leaf + n_big);
-        for (size_t i = 0; i < n_leaf; ++i)
-            pos_scene[i] = b.order[i];
-        for (size_t i = 0; i < n_big; ++i)
-            pos_scene[n_leaf + i] = b.big[i];
-        if (pos_scene.size() != n_spheres) {
-            ptg_context_destroy(ctx);
-            return fail(PTG_ERR_INVALID_ARGUMENT, "BVH: leaves and huge spheres do not cover the scene");
-        }
-        std::memcpy(blob.data() + off_pid, pos_scene.data(), pos_scene.size() * sizeof(int));
-#if PTG_BVH_POS_WINNER
-        {  // the shading records in position order: the winner's position indexes them directly
-            std::vector<ShadeRec> sp(n_spheres);
-            for (size_t i = 0; i < n_spheres; ++i)
-                sp[i] = shade[pos_scene[i]];
-            PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade, sp.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
-        }
-#endif
         if (hipMalloc(&ctx->d_bvh, total) != hipSuccess) {
             ptg_context_destroy(ctx);
             return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the BVH failed");
@@ -2863,8 +2801,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         A.bvh_id = reinterpret_cast<const int *>(base + off_id);
         A.big_geo = reinterpret_cast<const GeoRec *>(base + off_bgeo);
         A.big_id = reinterpret_cast<const int *>(base + off_bid);
-        A.pos_id = reinterpret_cast<const int *>(base + off_pid);
-        A.n_leaf = (int)n_leaf;
         A.n_nodes = (int)n_recs;
         A.n_big = (int)n_big;
     }

@@ -38,7 +38,8 @@ def main(src, tag, kernel_sub="render_kernel"):
     ks = list(csv.DictReader(open(stats)))
     out["kernel_stats"] = [{"name": r["Name"][:90], "calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                             "pct": float(r["Percentage"])} for r in ks[:6]]
-    render = [r for r in ks if kernel_sub in r["Name"]]
+    # the timed kernel only: bench.py's untimed counting launch (render_kernel<true, ...>) also matches
+    render = [r for r in ks if kernel_sub in r["Name"] and "render_kernel<true" not in r["Name"]]
     calls = sum(int(r["Calls"]) for r in render)
     out["render_avg_ms"] = sum(float(r["TotalDurationNs"]) for r in render) / calls / 1e6
     fetch, _ = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), kernel_sub)
@@ -53,7 +54,12 @@ def main(src, tag, kernel_sub="render_kernel"):
     out["sq"] = sq
     vgpr = [r for r in rows if kernel_sub in r["Kernel_Name"] and "render_kernel<true" not in r["Kernel_Name"]]
     if vgpr:
-        out["vgpr"] = int(vgpr[0]["VGPR_Count"])
+        # rocprofv3's VGPR_Count field, as reported: on gfx950 it shows 32 for
+        # the linear render kernel, whose code object allocates 57 VGPRs
+        # (.vgpr_count in the ISA metadata; `make -C cpu-path-tracing_amd
+        # resource-usage`) -- the field is not the allocation, so it is
+        # recorded under its own name
+        out["vgpr_rocprof_field"] = int(vgpr[0]["VGPR_Count"])
         out["sgpr"] = int(vgpr[0]["SGPR_Count"])
         out["lds_bytes"] = int(vgpr[0]["LDS_Block_Size"])
     bench = os.path.join(src, "bench_trace.json")
