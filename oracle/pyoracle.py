@@ -209,6 +209,7 @@ def render_xs_rect(spheres, cam, W, H, samps, nsub=2, seed=0x5EED0001, cols=None
 # Mode B for the accurate fp32 operation (error decomposition only)
 BV_IEEE_SQRT, BV_IEEE_DIV, BV_LIBM_TRIG, BV_RENORM, BV_FULL_SCAN, BV_LEX = 1, 2, 4, 8, 16, 32
 BV_DISC_NAIVE = 64  # round 1's discriminant hb^2 - a c for small spheres (a formulation, not an approximation)
+BV_NAIVE_ROOTS = 128  # small spheres' roots (-hb -+ sqrt(disc)) / a (round 4: C3 RMSE 5e-5 -> 4.5e-4, not kept)
 BV_ALL = 63  # every approximation swapped for the accurate fp32 operation
 
 

@@ -97,3 +97,4 @@ def test_out_of_range_paths_are_counted():
     sp["emission"][5] = -9.0
     _, _, bad = po.render_xs_f32_count(sp, cam, 32, 24, 4)
     assert bad > 0
+
