@@ -588,9 +588,10 @@ def test_c5_frame_size_rows_are_exact():
 @pytest.mark.parametrize("samps", [8, 37])
 def test_bvh_pixel_split_tail_is_exact(samps):
     """The BVH kernel's split tail (fill_launch, PTG_BVH_TAIL_PSPLIT): the
-    last ~round of rows runs each 16-pixel group as 4 (8 for 8-way splits)
-    units of interleaved pixels with every sample (resolved in the wave, no
-    HBM accumulation) -- the frame
+    last rows (PTG_BVH_TAIL_HALF_ROUNDS half rounds of wave slots) run each
+    16-pixel group as 8 units of 2 interleaved pixels (PTG_BVH_TAIL_CHUNKS_MANY
+    at this frame's >= 5 rounds, PTG_TAIL_CHUNKS below: both 8) with every
+    sample (resolved in the wave, no HBM accumulation) -- the frame
     equals the same frame in explicit sample chunks, and oracle rows of the
     tail (y = 0, 1) and the head equal the oracle's linear scan."""
     _require_gpu()
