@@ -191,6 +191,16 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // [0] main-loop iterations, [1] scans, [2] small-sphere root parts, [3] extra box-mode walls,
 // [4] diffuse/dielectric blocks, [5] mirror blocks, [6] refill batches, [7] small-sphere pre-tests
 __device__ unsigned long long ptg_dbg_stats[256 * 16];
+// PTG_BLOCK_STATS == 3: wave cycles inside the linear kernel's refill batch --
+// [0] batches, [1] flush + park of finished paths, [2] camera rays (ray_of),
+// [3] begin / store_pre
+__device__ unsigned long long ptg_dbg_stats2[256 * 16];
+#define PTG_SUB_T(var) const unsigned long long var = clock64()
+#define PTG_SUB_ADD(i, v)                                                                              \
+    do {                                                                                               \
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                                        \
+            atomicAdd(&ptg_dbg_stats2[(blockIdx.x & 255) * 16 + (i)], (v));                           \
+    } while (0)
 #define PTG_STAT(i)                                                                                    \
     do {                                                                                               \
         if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                                        \
@@ -1653,12 +1663,19 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             const int nn = (int)__popcll(need);
             if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
                 PTG_STAT(6);
+#if PTG_BLOCK_STATS == 3
+                PTG_SUB_T(rf_t0);
+#endif
                 const bool idle = waiting || item < 0;
                 if (parked)
                     flush_parked();
                 if (waiting)
                     park();
                 waiting = false;
+#if PTG_BLOCK_STATS == 3
+                PTG_SUB_T(rf_t1);
+                unsigned long long rf_ray = 0;
+#endif
                 if (!has_pre) {
                     // lanes of need below this one (v_mbcnt: no 64-bit lane mask held in VGPRs)
                     const int ni = next + (int)__builtin_amdgcn_mbcnt_hi(
@@ -1666,7 +1683,13 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     if (ni < total) {
                         f3 ro, rd;
                         uint32_t rs;
+#if PTG_BLOCK_STATS == 3
+                        PTG_SUB_T(rr_t0);
+#endif
                         ray_of(ni, ro, rd, rs);
+#if PTG_BLOCK_STATS == 3
+                        rf_ray = clock64() - rr_t0;
+#endif
                         if (idle) {  // idle lane: start it now (its record may hold a parked path)
                             begin(ni, ro, rd, rs);
                         } else {
@@ -1676,6 +1699,18 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     }
                 }
                 next += nn;
+#if PTG_BLOCK_STATS == 3
+                {
+                    const unsigned long long rf_t2 = clock64();
+                    unsigned long long ray_max = rf_ray;  // the wave's camera-ray time: its slowest lane's span
+                    for (int off = 32; off > 0; off >>= 1)
+                        ray_max = max(ray_max, (unsigned long long)__shfl_xor(ray_max, off, 64));
+                    PTG_SUB_ADD(0, 1ull);
+                    PTG_SUB_ADD(1, rf_t1 - rf_t0);
+                    PTG_SUB_ADD(2, ray_max);
+                    PTG_SUB_ADD(3, (rf_t2 - rf_t1) - ray_max);
+                }
+#endif
             }
         } else if (waiting) {  // pool exhausted: nothing left for this lane
             flush(E.x, E.y, E.z, slot);
@@ -2587,6 +2622,20 @@ int ptg_abi_version(void) { return PTG_ABI_VERSION; }
 
 #if PTG_BLOCK_STATS
 // debug builds only: the 16 block counters summed over their 256 slots (then zeroed)
+int ptg_debug_stats2_(unsigned long long *out16)
+{
+    std::vector<unsigned long long> h(256 * 16);
+    PTG_HIP(hipDeviceSynchronize());
+    PTG_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(ptg_dbg_stats2), h.size() * sizeof(h[0])));
+    for (int i = 0; i < 16; ++i) {
+        out16[i] = 0;
+        for (int b = 0; b < 256; ++b)
+            out16[i] += h[b * 16 + i];
+    }
+    std::vector<unsigned long long> z(h.size(), 0ull);
+    PTG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ptg_dbg_stats2), z.data(), z.size() * sizeof(z[0])));
+    return PTG_OK;
+}
 int ptg_debug_stats_(unsigned long long *out16)
 {
     std::vector<unsigned long long> h(256 * 16);

@@ -41,3 +41,11 @@ print(sys.argv[2], scene, "wave cycles per 64 lane-segments:",
 if not scene.startswith("synthetic"):  # PTG_BLOCK_STATS=3: the diffuse/dielectric block inside shade
     print(f"  of which the diffuse/dielectric block: {64 * st[14] / lane_segs:.0f} ({100 * st[14] / tot:.1f} %)")
     print(f"  box mode's extra-wall block (in scan): {64 * st[15] / lane_segs:.0f} ({100 * st[15] / tot:.1f} %)")
+if not scene.startswith("synthetic") and hasattr(ptgpu.lib(), "ptg_debug_stats2_"):
+    s2 = (C.c_ulonglong * 16)()
+    # (the refill sub-phases were accumulated by the same render; read them now)
+    ptgpu.lib().ptg_debug_stats2_(s2)
+    nb = max(1, s2[0])
+    print(f"  refill batches {s2[0]} ({64 * s2[0] / lane_segs:.3f} per 64 lane-segments): per batch flush+park "
+          f"{s2[1] / nb:.0f}, camera rays {s2[2] / nb:.0f}, begin/store {s2[3] / nb:.0f} wave cycles; per 64 "
+          f"lane-segments {64 * s2[1] / lane_segs:.0f} / {64 * s2[2] / lane_segs:.0f} / {64 * s2[3] / lane_segs:.0f}")
