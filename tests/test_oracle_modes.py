@@ -116,3 +116,22 @@ def test_rect_renders_equal_row_renders(name, W, H, samps, rows, cols):
         mask = np.ones((H, W), bool)
         mask[np.ix_(ys, np.arange(*cols))] = False
         assert (r[mask] == 0).all() and r[~mask].sum() > 0
+
+
+def test_mode_b_output_is_pinned():
+    """The checker itself is pinned: Mode B frames -- the fp32
+    restatement the GPU's exact mode must equal bit for bit -- against the
+    values stored by oracle/gen_mode_b_pin.py, so a change of compiler or
+    flags in oracle/Makefile (-O3, -mfma, -ffp-contract=off) cannot move the
+    oracle without this test failing."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import gen_mode_b_pin as g
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mode_b_pin.npz"),
+                allow_pickle=False)
+    for name, W, H, samps in g.CASES:
+        img, segs = g.frame(name, W, H, samps)
+        key = name.replace(":", "_")
+        assert np.array_equal(img, z[key]), name
+        assert segs == int(z[key + "_segments"]), name
