@@ -18,7 +18,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
-#include <cstring>
 #include <vector>
 
 #include "../../include/ptgpu.h"
@@ -557,136 +556,6 @@ inline std::vector<int32_t> wide_conts(const std::vector<BvhNodeQ> &w, int32_t b
     std::vector<int32_t> out(w.size() / kWide, -1);
     if (!w.empty())
         detail::wide_conts_rec(w, base, 0, -1, out);
-    return out;
-}
-
-// Compressed 4-wide layout (ptg_render.hip PTG_BVH_Q8): 48 B per wide node --
-// three 16-B loads per node step instead of four (the BVH kernel is bound by
-// the vector-memory data path: TD busy 94 % of cycles at C5, profiles/
-// r04_vmem_c5.txt).  The same nodes, in the same depth-first order and with
-// the same positions (node index * 4 + slot, so wide_conts of the 64-B layout
-// applies) as wide_bvh; per node, 12 dwords:
-//   d0-d2  the node's box, binary16 on the WideGrid, near-plane first for the
-//          octant (d0 = {near x, near y}, d1 = {near z, far x}, d2 = {far y,
-//          far z}), rounded outward; it is the union of the children's boxes;
-//   d3-d8  the children's planes, 8 bits each, as fractions of the node box
-//          along each axis in the octant's orientation (0: the node's near
-//          plane, 255: its far plane), near planes rounded toward the node's
-//          near plane, far planes toward its far plane; d3 = near x, d4 = near
-//          y, d5 = near z, d6 = far x, d7 = far y, d8 = far z, child k in byte k
-//          (an empty slot: near 255, far 0 -- the octant's rays miss it);
-//   d9-d11 four 24-bit child words, child k at bits 24k of the 96-bit field:
-//          a node's position (< 2^23), or a leaf 0x800000 | (count - 0) << 20 |
-//          first (first < 2^20, count <= 7; an empty slot: count 0).
-// The kernel decodes a plane's slab time as t_near + q (t_far - t_near) / 255
-// (affine in the plane value); the quantisation keeps a 1e-3-step margin
-// outward, and the boxes' own padding (1e-4 (extent + |coordinate| + 1))
-// stays far above the fp32 rounding of that interpolation.
-struct WideQ8Node {
-    uint32_t d[12];
-};
-static_assert(sizeof(WideQ8Node) == 48, "compressed wide node is three float4");
-
-// the 24-bit words' limits
-inline bool wide_q8_supported(const BvhBuild &b, size_t positions_total)
-{
-    if (positions_total >= (size_t(1) << 23))
-        return false;
-    for (const BvhNodeHost &n : b.nodes)
-        if (n.leaf >= 0 && ((n.leaf & 0xFFFFFF) >= (1 << 20) || (n.leaf >> 24) > 7))
-            return false;
-    return true;
-}
-
-namespace detail {
-
-inline int wide_q8_rec(const BvhBuild &b, int i, int octant, const WideGrid &z, int32_t base,
-                       std::vector<WideQ8Node> &out)
-{
-    const int me = (int)out.size();
-    int kids[kWide], nk = 0;
-    if (b.nodes[i].leaf >= 0) {
-        kids[0] = i;
-        nk = 1;
-    } else {
-        wide_children(b, i, octant, kids, nk);
-    }
-    out.resize(me + 1);
-    // the node box: the union of the children's boxes, binary16 outward
-    BvhNodeHost u = b.nodes[kids[0]];
-    for (int k = 1; k < nk; ++k)
-        for (int c = 0; c < 3; ++c) {
-            u.bmin[c] = std::min(u.bmin[c], b.nodes[kids[k]].bmin[c]);
-            u.bmax[c] = std::max(u.bmax[c], b.nodes[kids[k]].bmax[c]);
-        }
-    uint16_t lo16[3], hi16[3];
-    double lo[3], hi[3];
-    for (int c = 0; c < 3; ++c) {
-        lo16[c] = z.plane(u.bmin[c], c, -1);
-        hi16[c] = z.plane(u.bmax[c], c, +1);
-        lo[c] = (double)z.centre[c] + half_value(lo16[c]) * (double)z.scale[c];
-        hi[c] = (double)z.centre[c] + half_value(hi16[c]) * (double)z.scale[c];
-    }
-    uint32_t near16[3], far16[3];
-    double nearv[3], farv[3];
-    for (int c = 0; c < 3; ++c) {
-        const bool f = (octant >> c) & 1;
-        near16[c] = f ? hi16[c] : lo16[c];
-        far16[c] = f ? lo16[c] : hi16[c];
-        nearv[c] = f ? hi[c] : lo[c];
-        farv[c] = f ? lo[c] : hi[c];
-    }
-    uint32_t d[12] = {near16[0] | (near16[1] << 16), near16[2] | (far16[0] << 16), far16[1] | (far16[2] << 16)};
-    uint32_t words[kWide];
-    for (int k = 0; k < kWide; ++k) {
-        // an empty slot by default
-        for (int c = 0; c < 3; ++c) {
-            d[3 + c] |= 255u << (8 * k);
-            d[6 + c] |= 0u << (8 * k);
-        }
-        words[k] = 0x800000u;
-    }
-    for (int k = 0; k < nk; ++k) {
-        const BvhNodeHost &ch = b.nodes[kids[k]];
-        for (int c = 0; c < 3; ++c) {
-            const bool f = (octant >> c) & 1;
-            const double cn = f ? (double)ch.bmax[c] : (double)ch.bmin[c];
-            const double cf = f ? (double)ch.bmin[c] : (double)ch.bmax[c];
-            const double span = farv[c] - nearv[c];
-            int qn = 0, qf = 255;
-            if (span != 0.0) {
-                qn = (int)std::floor((cn - nearv[c]) / span * 255.0 - 1e-3);
-                qf = (int)std::ceil((cf - nearv[c]) / span * 255.0 + 1e-3);
-            }
-            qn = std::max(0, std::min(255, qn));
-            qf = std::max(0, std::min(255, qf));
-            d[3 + c] &= ~(255u << (8 * k));
-            d[3 + c] |= (uint32_t)qn << (8 * k);
-            d[6 + c] |= (uint32_t)qf << (8 * k);
-        }
-        if (ch.leaf >= 0)
-            words[k] = 0x800000u | ((uint32_t)(ch.leaf >> 24) << 20) | (uint32_t)(ch.leaf & 0xFFFFF);
-        else
-            words[k] = (uint32_t)(base + 4 * wide_q8_rec(b, kids[k], octant, z, base, out)) & 0xFFFFFFu;
-    }
-    d[9] = words[0] | (words[1] << 24);
-    d[10] = (words[1] >> 8) | (words[2] << 16);
-    d[11] = (words[2] >> 16) | (words[3] << 8);
-    std::memcpy(out[me].d, d, sizeof(d));
-    return me;
-}
-
-}  // namespace detail
-
-// The compressed layout of the tree for rays of one octant (node positions
-// offset by `base`, in record units: base + 4 * node).
-inline std::vector<WideQ8Node> wide_bvh_q8(const BvhBuild &b, int octant, int32_t base)
-{
-    std::vector<WideQ8Node> out;
-    if (b.nodes.empty())
-        return out;
-    const WideGrid z(b.nodes[0]);
-    detail::wide_q8_rec(b, 0, octant, z, base, out);
     return out;
 }
 

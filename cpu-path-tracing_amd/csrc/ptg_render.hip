@@ -180,28 +180,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BVH_LDS_ROOT
 #define PTG_BVH_LDS_ROOT 0  // A/B: the root wide node of every octant layout read from LDS
 #endif
-#ifndef PTG_BVH_Q8
-// BVH (wide walk): compressed 48-B nodes (bvh_build.hpp WideQ8Node: the node
-// box in binary16, the children's planes as 8-bit fractions of it, 24-bit
-// child words) -- three 16-B loads per node step instead of four.  The BVH
-// kernel is bound by the vector-memory data path (TD busy 94 % of cycles at
-// C5, profiles/r04_vmem_c5.txt), not by its VALU (68 % issue).
-#define PTG_BVH_Q8 0
-#endif
-// Parked-leaf words: the leaf's first sphere and count.  Wide words are
-// INT_MIN | count << 24 | first; compressed (PTG_BVH_Q8) words are 24-bit,
-// sign-extended: 0xFF800000 | count << 20 | first.
-#if PTG_BVH_Q8 && PTG_BVH_WIDE
-#define PEND_OF_WORD(w) ((w) & 0x7FFFFF)
-#define PEND_FIRST(p) ((p) & 0xFFFFF)
-#define PEND_COUNT(p) ((p) >> 20)
-#define PEND_MAKE(f, c) ((f) | ((c) << 20))
-#else
-#define PEND_OF_WORD(w) ((w) & 0x7FFFFFFF)
-#define PEND_FIRST(p) ((p) & 0xFFFFFF)
-#define PEND_COUNT(p) ((p) >> 24)
-#define PEND_MAKE(f, c) ((f) | ((c) << 24))
-#endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
                           // (measured with octant layouts + SAH: 6 beats 4 by 7 %, 5 and 7 by 1-2 %)
@@ -803,7 +781,6 @@ __device__ __forceinline__ void update_lex(const float t, const int sid, float &
 template <class T>
 using gptr = const T __attribute__((address_space(1))) *;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // a compact node record, loadable from gptr
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 struct BvhTrav {
     int ni;    // binary: next node in depth-first order; wide: see below
@@ -969,46 +946,6 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
                                               int shift = 0)
 {
     const int base = tr.ni & ~3;
-#if PTG_BVH_Q8
-    // compressed node (bvh_build.hpp WideQ8Node): three 16-B loads
-    const gptr<u32x4> qn = qnodes + (base >> 2) * 3;
-    const u32x4 h = qn[0], pl = qn[1], wd = qn[2];
-    if constexpr (kCount)
-        cnt.boxes += 4 - (tr.ni & 3);
-    const float tcap = tr.tb * 1.0001f;
-    // the node box's slab times (near planes, far planes), and per axis the
-    // step of one 1/255 of it
-    const float tnx = __builtin_fmaf(lo_half(h.x), r.sx, r.bx);
-    const float tny = __builtin_fmaf(hi_half(h.x), r.sy, r.by);
-    const float tnz = __builtin_fmaf(lo_half(h.y), r.sz, r.bz);
-    const float stx = (__builtin_fmaf(hi_half(h.y), r.sx, r.bx) - tnx) * (1.0f / 255.0f);
-    const float sty = (__builtin_fmaf(lo_half(h.z), r.sy, r.by) - tny) * (1.0f / 255.0f);
-    const float stz = (__builtin_fmaf(hi_half(h.z), r.sz, r.bz) - tnz) * (1.0f / 255.0f);
-    auto ub = [](unsigned w, int k) { return (float)((w >> (8 * k)) & 0xFFu); };  // v_cvt_f32_ubyteK
-    auto child = [&](int k) {
-        const float ax = __builtin_fmaf(ub(h.w, k), stx, tnx), ay = __builtin_fmaf(ub(pl.x, k), sty, tny),
-                    az = __builtin_fmaf(ub(pl.y, k), stz, tnz);
-        const float bx = __builtin_fmaf(ub(pl.z, k), stx, tnx), by = __builtin_fmaf(ub(pl.w, k), sty, tny),
-                    bz = __builtin_fmaf(ub(wd.x, k), stz, tnz);
-        const float t_in = __builtin_fmaxf(__builtin_fmaxf(ax, ay), __builtin_fmaxf(az, 0.0f));
-        const float t_out = __builtin_fminf(__builtin_fminf(bx, by), __builtin_fminf(bz, tcap));
-        return !(t_in > t_out);
-    };
-    const unsigned m = ((child(0) ? 1u : 0u) | (child(1) ? 2u : 0u) | (child(2) ? 4u : 0u) | (child(3) ? 8u : 0u)) &
-                       (0xFu << (tr.ni & 3));
-    // 24-bit words, sign-extended (leaves negative, positions >= 0)
-    auto sx24 = [](unsigned v) { return ((int)(v << 8)) >> 8; };
-    // held as a vector: four scalar locals selected through a by-reference
-    // lambda became a select of their addresses and a scratch round trip
-    const i32x4 ws4 = {sx24(wd.y), sx24(__builtin_amdgcn_alignbit(wd.z, wd.y, 24)),
-                       sx24(__builtin_amdgcn_alignbit(wd.w, wd.z, 16)), ((int)wd.w) >> 8};
-    auto lowest = [ws4](unsigned x) {
-        int w = ws4.w;
-        w = (x & 4u) ? ws4.z : w;
-        w = (x & 2u) ? ws4.y : w;
-        return (x & 1u) ? ws4.x : w;
-    };
-#else
     u32x4 q0, q1, q2, q3;
 #if PTG_BVH_LDS_ROOT
     if (lds_root && (base & root_mask) == 0) {  // a layout's root: staged in LDS
@@ -1025,14 +962,6 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
         q1 = q[1];
         q2 = q[2];
         q3 = q[3];
-#if PTG_TD_PROBE  // timing probe only: PTG_TD_PROBE extra 16-B loads of the same line per node step (same results)
-        for (int k = 0; k < PTG_TD_PROBE; ++k) {
-            u32x4 x;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(q + (k & 3)) : "memory");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            asm volatile("" ::"v"(x));
-        }
-#endif
     }
     if constexpr (kCount)
         cnt.boxes += 4 - (tr.ni & 3);
@@ -1047,13 +976,12 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
         w = (x & 2u) ? (int)q1.w : w;
         return (x & 1u) ? (int)q0.w : w;
     };
-#endif
     const unsigned r1 = m & (m - 1u);  // hits after the first
     const int wf = lowest(m), ws = lowest(r1);
     const bool leaf = (m != 0u) & (wf < kPopLater);  // the first hit is a leaf: parked
     const unsigned rest = leaf ? r1 & (r1 - 1u) : r1;
     int next = m == 0u ? -1 : leaf ? (r1 != 0u ? ws : kPopLater) : wf;
-    tr.pend = leaf ? PEND_OF_WORD(wf) : tr.pend;
+    tr.pend = leaf ? (wf & 0x7FFFFFFF) : tr.pend;
     const int pos = base + (int)__builtin_ctz(rest | 16u);
     const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
 #if PTG_BVH_STACK >= 3
@@ -1073,7 +1001,7 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     if (next == -1) {
         next = bvh_pop(cont, tr);
         if (next < kPopLater) {  // a leaf from the stack
-            tr.pend = PEND_OF_WORD(next);
+            tr.pend = next & 0x7FFFFFFF;
             next = kPopLater;
         }
     }
@@ -1114,7 +1042,7 @@ __device__ __forceinline__ void bvh_leaf_done_sel(gptr<int> cont, BvhTrav &tr, c
     tr.pend = act ? -1 : tr.pend;
     int next = bvh_pop_sel(cont, tr, act & (tr.ni == kPopLater), tr.ni);
     const bool lf = act & (next < kPopLater);  // a leaf word (popped, or waiting in ni)
-    tr.pend = lf ? PEND_OF_WORD(next) : tr.pend;
+    tr.pend = lf ? (next & 0x7FFFFFFF) : tr.pend;
     next = lf ? kPopLater : next;
     tr.ni = act ? next : tr.ni;
 }
@@ -1161,7 +1089,7 @@ __device__ __forceinline__ void bvh_leaf_done(gptr<int> cont, BvhTrav &tr)
     if (tr.ni < -1) {  // kPopLater, or the leaf the node step moved to after parking one
         int next = tr.ni == kPopLater ? bvh_pop(cont, tr) : tr.ni;
         if (next < kPopLater) {  // a leaf: parked for the next leaf phase
-            tr.pend = PEND_OF_WORD(next);
+            tr.pend = next & 0x7FFFFFFF;
             next = kPopLater;
         }
         tr.ni = next;
@@ -1175,7 +1103,7 @@ __device__ __forceinline__ void bvh_leaf_done(gptr<int> cont, BvhTrav &tr)
 template <bool kCount, bool kExact>
 __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
-    const int first = PEND_FIRST(tr.pend), nl = PEND_COUNT(tr.pend);
+    const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
 #if PTG_LEAF_CHUNK > 0
     // at most PTG_LEAF_CHUNK spheres per leaf phase; the rest stays parked
     const int take = nl < PTG_LEAF_CHUNK ? nl : PTG_LEAF_CHUNK;
@@ -1184,7 +1112,7 @@ __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f
 #endif
     leaf_spheres<kCount, kExact>(A, first, take, o, d, tr.tb, tr.best, cnt);
     if (take < nl) {
-        tr.pend = PEND_MAKE(first + take, nl - take);
+        tr.pend = (first + take) | ((nl - take) << 24);
         return;
     }
     bvh_leaf_done(cont, tr);
@@ -1205,7 +1133,7 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
                                                uint8_t (*pair)[64])
 {
     const int lane = (int)__lane_id();
-    const int nl = has ? PEND_COUNT(tr.pend) : 0;
+    const int nl = has ? (tr.pend >> 24) : 0;
     const bool own = nl >= 2, hlp = !has;
     auto rank = [](unsigned long long m) {
         return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -1245,7 +1173,7 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     const int ppend = bpi(partner, tr.pend);
     const f3 ro3 = ph ? po3 : o, rd3 = ph ? pd3 : d;
     const int pendl = ph ? ppend : tr.pend;
-    const int first = PEND_FIRST(pendl), nll = PEND_COUNT(pendl);
+    const int first = pendl & 0xFFFFFF, nll = pendl >> 24;
     // the leaf's parts: one helper -> [0, ceil(n/2)), [ceil(n/2), n); two
     // helpers -> [0, n/3), [n/3, 2n/3), [2n/3, n) (n <= 12: x/3 = x*11 >> 5)
     const int k = ph ? 1 + (orank < np2) : po ? 1 + (ro < np2) : 0;
@@ -2860,16 +2788,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
 #endif
         const size_t stride = size_t(1) << shift;
-#if PTG_BVH_WIDE && PTG_BVH_Q8
-        // compressed nodes: stride / 4 nodes of 48 B per layout
-        if (!wide_q8_supported(b, n_layouts * stride)) {
-            ptg_context_destroy(ctx);
-            return fail(PTG_ERR_UNSUPPORTED, "BVH: the scene exceeds the compressed nodes' 24-bit words");
-        }
-        const size_t off_cont = off_q + n_layouts * (stride / kWide) * sizeof(WideQ8Node);
-#else
         const size_t off_cont = off_q + n_layouts * stride * sizeof(BvhNodeQ);
-#endif
         const size_t total = off_cont + (PTG_BVH_WIDE ? n_layouts * stride / kWide * sizeof(int32_t) : 0) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
@@ -2889,19 +2808,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
                 if (z.word >= 0)
                     z.word += (int32_t)(k * stride);  // absolute skip index
 #endif
-#if PTG_BVH_WIDE && PTG_BVH_Q8
-            {
-                const std::vector<WideQ8Node> q8 = wide_bvh_q8(b, (int)k, (int32_t)(k * stride));
-                if (q8.size() * kWide != n_recs) {
-                    ptg_context_destroy(ctx);
-                    return fail(PTG_ERR_INVALID_ARGUMENT, "BVH: compressed layout size mismatch");
-                }
-                std::memcpy(blob.data() + off_q + k * (stride / kWide) * sizeof(WideQ8Node), q8.data(),
-                            q8.size() * sizeof(WideQ8Node));
-            }
-#else
             std::memcpy(blob.data() + off_q + k * stride * sizeof(BvhNodeQ), qk.data(), n_recs * sizeof(BvhNodeQ));
-#endif
         }
         A.bvh_shift = shift;
         A.bvh_mask = (int)(stride - 1);

@@ -133,66 +133,6 @@ static void wide_walk(const std::vector<ptg_sphere> &s, const BvhBuild &b, const
     CHECK(used >= 1, "octant %d node %d has no children", octant, node);
 }
 
-// the compressed layout (wide_bvh_q8) against the 64-B one: the same nodes
-// at the same positions, equal child words, and each child's 8-bit box
-// (decoded on its node's binary16 box) containing its subtree's spheres
-static void q8_walk(const std::vector<ptg_sphere> &s, const BvhBuild &b, const WideGrid &g,
-                    const std::vector<WideQ8Node> &q, const std::vector<BvhNodeQ> &w, int32_t base, int node,
-                    std::vector<int> &slots, int octant)
-{
-    CHECK(node >= 0 && node % kWide == 0 && node / kWide < (int)q.size(), "q8 octant %d node %d", octant, node);
-    const uint32_t *d = q[node / kWide].d;
-    double nearv[3], farv[3];
-    const uint16_t n16[3] = {(uint16_t)(d[0] & 0xFFFFu), (uint16_t)(d[0] >> 16), (uint16_t)(d[1] & 0xFFFFu)};
-    const uint16_t f16[3] = {(uint16_t)(d[1] >> 16), (uint16_t)(d[2] & 0xFFFFu), (uint16_t)(d[2] >> 16)};
-    for (int c = 0; c < 3; ++c) {
-        nearv[c] = g.centre[c] + half_value(n16[c]) * (double)g.scale[c];
-        farv[c] = g.centre[c] + half_value(f16[c]) * (double)g.scale[c];
-        CHECK((octant >> c) & 1 ? nearv[c] >= farv[c] : nearv[c] <= farv[c], "q8 octant %d node %d axis %d not near-first",
-              octant, node, c);
-    }
-    const uint32_t words[kWide] = {d[9] & 0xFFFFFFu, (d[9] >> 24) | ((d[10] & 0xFFFFu) << 8),
-                                   (d[10] >> 16) | ((d[11] & 0xFFu) << 16), d[11] >> 8};
-    for (int k = 0; k < kWide; ++k) {
-        const BvhNodeQ &r = w[node + k];
-        unsigned qn[3], qf[3];
-        for (int c = 0; c < 3; ++c) {
-            qn[c] = (d[3 + c] >> (8 * k)) & 0xFFu;
-            qf[c] = (d[6 + c] >> (8 * k)) & 0xFFu;
-        }
-        if (r.word == kWideEmpty) {
-            CHECK(words[k] == 0x800000u && qn[0] == 255 && qn[1] == 255 && qn[2] == 255 && qf[0] == 0 && qf[1] == 0 &&
-                      qf[2] == 0,
-                  "q8 octant %d node %d: empty slot %d", octant, node, k);
-            continue;
-        }
-        std::vector<int> sub;
-        if (r.word < 0) {
-            const int leaf = r.word & 0x7FFFFFFF, first = leaf & 0xFFFFFF, cnt = leaf >> 24;
-            CHECK(words[k] == (0x800000u | (uint32_t)cnt << 20 | (uint32_t)first), "q8 octant %d node %d leaf word %d",
-                  octant, node, k);
-            for (int j = first; j < first + cnt; ++j)
-                sub.push_back(j);
-        } else {
-            CHECK(words[k] == (uint32_t)r.word, "q8 octant %d node %d child word %d", octant, node, k);
-            q8_walk(s, b, g, q, w, base, r.word - base, sub, octant);
-            if (fails)
-                return;
-        }
-        for (int j : sub) {
-            const ptg_sphere &sp = s[b.order[j]];
-            for (int c = 0; c < 3; ++c) {
-                const double a = nearv[c] + qn[c] / 255.0 * (farv[c] - nearv[c]);
-                const double e = nearv[c] + qf[c] / 255.0 * (farv[c] - nearv[c]);
-                CHECK(std::min(a, e) <= sp.position[c] - sp.radius && std::max(a, e) >= sp.position[c] + sp.radius,
-                      "q8 octant %d node %d slot %d does not contain sphere %d (axis %d)", octant, node, k, b.order[j],
-                      c);
-            }
-        }
-        slots.insert(slots.end(), sub.begin(), sub.end());
-    }
-}
-
 static void check_wide(const std::vector<ptg_sphere> &s, const BvhBuild &b)
 {
     if (b.nodes.empty()) {  // every sphere huge: no tree, no wide layout
@@ -208,13 +148,6 @@ static void check_wide(const std::vector<ptg_sphere> &s, const BvhBuild &b)
         wide_walk(s, b, g, w, base, 0, cover, slots, oct);
         for (size_t k = 0; k < cover.size() && !fails; ++k)
             CHECK(cover[k] == 1, "octant %d wide: leaf slot %zu reached %d times", oct, k, cover[k]);
-        if (!fails && wide_q8_supported(b, 8 * w.size())) {
-            const std::vector<WideQ8Node> q = wide_bvh_q8(b, oct, base);
-            CHECK(q.size() * kWide == w.size(), "q8 octant %d: %zu nodes for %zu records", oct, q.size(), w.size());
-            std::vector<int> qslots;
-            q8_walk(s, b, g, q, w, base, 0, qslots, oct);
-            CHECK(fails || qslots == slots, "q8 octant %d: leaf order differs from the 64-B layout", oct);
-        }
         // continuations: a walk that enters every child and moves on only by
         // next-slot / continuation (the kernel's overflow fallback) reaches
         // every leaf once, in depth-first order
