@@ -177,6 +177,12 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_BOX_MODE
 #define PTG_BOX_MODE 1  // linear scenes: nearest-plane wall first (box mode, scene_scan)
 #endif
+#ifndef PTG_NODE_CASCADE
+#define PTG_NODE_CASCADE 1  // BVH node step: the first hits' words and slots by a select cascade on the box tests
+#endif
+#ifndef PTG_NODE_OFS32
+#define PTG_NODE_OFS32 1  // BVH node loads: 32-bit offsets on the SGPR base
+#endif
 #ifndef PTG_BVH_LDS_ROOT
 #define PTG_BVH_LDS_ROOT 0  // A/B: the root wide node of every octant layout read from LDS
 #endif
@@ -957,7 +963,13 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     } else
 #endif
     {
+#if PTG_NODE_OFS32
+        // a 32-bit byte offset on the uniform base: the load's saddr form
+        // (no 64-bit address arithmetic per lane)
+        gptr<u32x4> q = (gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + ((unsigned)base << 4));
+#else
         gptr<u32x4> q = qnodes + base;
+#endif
         q0 = q[0];
         q1 = q[1];
         q2 = q[2];
@@ -966,6 +978,40 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     if constexpr (kCount)
         cnt.boxes += 4 - (tr.ni & 3);
     const float tcap = tr.tb * 1.0001f;
+#if PTG_NODE_CASCADE
+    // slots before the walk's position (ni & 3) are not tested again
+    const int s = tr.ni & 3;
+    const bool h0 = box_hit_sorted(q0, r, tcap) & (s == 0), h1 = box_hit_sorted(q1, r, tcap) & (s <= 1),
+               h2 = box_hit_sorted(q2, r, tcap) & (s <= 2), h3 = box_hit_sorted(q3, r, tcap);
+    // the words of the first three hits in slot order (-1: none) and the
+    // slots of the second and third, shifted in from the last slot: every
+    // step is a v_cndmask on its box test's lane mask (the hit mask with
+    // lowest-set-bit lookups took 10-16 VALU more per node step: C5 +4.8 %)
+    int w1 = h3 ? (int)q3.w : -1, w2 = -1, w3 = -1;
+    w2 = h2 ? w1 : w2;
+    w1 = h2 ? (int)q2.w : w1;
+    w3 = h1 ? w2 : w3;
+    w2 = h1 ? w1 : w2;
+    w1 = h1 ? (int)q1.w : w1;
+    w3 = h0 ? w2 : w3;
+    w2 = h0 ? w1 : w2;
+    w1 = h0 ? (int)q0.w : w1;
+    int i2 = 3, i3 = 3;  // (meaningful only where the hit exists)
+    i3 = h1 ? i2 : i3;
+    i2 = h1 ? (h2 ? 2 : 3) : i2;
+    i3 = h0 ? i2 : i3;
+    i2 = h0 ? (h1 ? 1 : h2 ? 2 : 3) : i2;
+    const bool leaf = w1 < kPopLater;  // the first hit is a leaf: parked (no hit: w1 = -1)
+    int next = leaf ? (w2 != -1 ? w2 : kPopLater) : w1;
+    tr.pend = leaf ? (w1 & 0x7FFFFFFF) : tr.pend;
+    // the hits left after next: from the second (an inner first hit) or the
+    // third (a parked leaf); one goes on the stack as its word, several as
+    // the position of the first of them
+    const bool push = leaf ? w3 != -1 : w2 != -1;
+    const bool several = leaf ? (h0 & h1 & h2 & h3) : w3 != -1;
+    const int pos = base + (leaf ? i3 : i2);
+    const int e = several ? pos : leaf ? w3 : w2;
+#else
     const unsigned m = ((box_hit_sorted(q0, r, tcap) ? 1u : 0u) | (box_hit_sorted(q1, r, tcap) ? 2u : 0u) |
                         (box_hit_sorted(q2, r, tcap) ? 4u : 0u) | (box_hit_sorted(q3, r, tcap) ? 8u : 0u)) &
                        (0xFu << (tr.ni & 3));
@@ -984,15 +1030,22 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     tr.pend = leaf ? (wf & 0x7FFFFFFF) : tr.pend;
     const int pos = base + (int)__builtin_ctz(rest | 16u);
     const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
+#endif
 #if PTG_BVH_STACK >= 3
-    const bool push = rest != 0u, full = tr.s2 != -1;
+#if !PTG_NODE_CASCADE
+    const bool push = rest != 0u;
+#endif
+    const bool full = tr.s2 != -1;
     tr.res = (push & full) ? pos : tr.res;
     const int s0 = tr.s0, s1 = tr.s1;
     tr.s0 = push ? (full ? -1 : e) : s0;
     tr.s1 = push ? (full ? -1 : s0) : s1;
     tr.s2 = push ? (full ? -1 : s1) : tr.s2;
 #else
-    const bool push = rest != 0u, full = tr.s1 != -1;
+#if !PTG_NODE_CASCADE
+    const bool push = rest != 0u;
+#endif
+    const bool full = tr.s1 != -1;
     tr.res = (push & full) ? pos : tr.res;
     const int s0 = tr.s0;
     tr.s0 = push ? (full ? -1 : e) : s0;
@@ -1073,11 +1126,23 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
     const float a = dot3(d, d);
     if constexpr (kCount)
         sc.spheres += cnt;
+#if PTG_NODE_OFS32
+    // 32-bit byte offsets on the uniform bases (saddr loads)
+    const char *sph = (const char *)A.bvh_sph;
+    const char *ids = (const char *)A.bvh_id;
+    for (int j = 0; j < cnt; ++j) {
+        const unsigned off = (unsigned)(f + j) << 4;
+        const float t = root_lex<false, kExact>(*(const float4 *)(sph + off), float4{}, o, d, a, tb);
+        if (t <= tb)  // the scene index is read only for a candidate that wins or ties
+            update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
+    }
+#else
     for (int j = 0; j < cnt; ++j) {
         const float t = root_lex<false, kExact>(A.bvh_sph[f + j], float4{}, o, d, a, tb);
         if (t <= tb)  // the scene index is read only for a candidate that wins or ties
             update_lex(t, A.bvh_id[f + j], tb, best);
     }
+#endif
 }
 
 // After the parked leaf's spheres: wide walk -- a leaf word waiting in tr.ni
