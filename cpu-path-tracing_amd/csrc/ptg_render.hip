@@ -1007,10 +1007,11 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     // the hits left after next: from the second (an inner first hit) or the
     // third (a parked leaf); one goes on the stack as its word, several as
     // the position of the first of them
+    // (each select on one lane mask: a select between two conditions was
+    // materialised as 5 VALU)
     const bool push = leaf ? w3 != -1 : w2 != -1;
-    const bool several = leaf ? (h0 & h1 & h2 & h3) : w3 != -1;
     const int pos = base + (leaf ? i3 : i2);
-    const int e = several ? pos : leaf ? w3 : w2;
+    const int e = leaf ? ((h0 & h1 & h2 & h3) ? pos : w3) : (w3 != -1 ? pos : w2);
 #else
     const unsigned m = ((box_hit_sorted(q0, r, tcap) ? 1u : 0u) | (box_hit_sorted(q1, r, tcap) ? 2u : 0u) |
                         (box_hit_sorted(q2, r, tcap) ? 4u : 0u) | (box_hit_sorted(q3, r, tcap) ? 8u : 0u)) &
