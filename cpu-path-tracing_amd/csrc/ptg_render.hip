@@ -583,7 +583,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // kn's wall is missing only when no existing wall the ray moves
         // toward has v > 0 (every such plane is parallel to the ray): then no
         // wall can be hit from inside the room, and the test is masked
-        const int in = walls[2 * kn + (comp(d, kn) >= 0.0f ? 0 : 1)];
+        // (the byte offset selected directly: an index select became a
+        // v_cndmask 0/1 and a shift)
+        const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls + 2 * kn) +
+                                                      (comp(d, kn) >= 0.0f ? 0 : 4));
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, kAxAny>{}, un, vn, in >= 0);
         const float bqm = bq * kPlaneMargin;
