@@ -716,9 +716,12 @@ struct ScanCount {
 // g0 = {P0, R}, g1 = {n0, 2R} (huge spheres); else g0 = {C, -R^2}.
 constexpr float kReject = __builtin_nanf("");  // every comparison with it is false
 
+// the cull's scaled culling distance: tb * -2 (1 + 2^-20), exact constant
+constexpr float kCullScale = -2.0f * kCullMargin;
+
 template <bool kBig, bool kExact>
 __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, const f3 o, const f3 d, const float a,
-                                          const float tb)
+                                          const float tb, const float tbm)
 {
     f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
     float ed = dot3(e, d);
@@ -733,8 +736,13 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
     }
     // the two culls and the discriminant test as one early-out (bitwise: the
     // && chains had been evaluated as nested exec-masked blocks; C5 -1.1 %)
-    const bool behind = (hb >= 0.0f) & (c >= 0.0f);
-    const bool beyond = (hb < 0.0f) & (c > 0.0f) & (c >= (tb * (-2.0f * hb)) * kCullMargin);  // near root > tb
+    // The two culls as one compare: behind (hb >= 0, c >= 0) and beyond (hb
+    // < 0, near root > tb: c >= 2 |hb| tb (1 + 2^-20); the margin covers the q
+    // bound's 3u and the two roundings) are c >= max(hb tbm, 0) with tbm = tb
+    // * kCullScale < 0 from the caller (once per change of tb): hb tbm <= 0
+    // for hb >= 0 (NaN for hb = 0, tb = inf: fmax gives 0), > 0 for hb < 0.
+    // (As two sign-selected compares the choice was materialised: 5 VALU.)
+    const bool culled = c >= __builtin_fmaxf(hb * tbm, 0.0f);
     float disc;
     if constexpr (kBig) {
         disc = __builtin_fmaf(hb, hb, -(a * c));
@@ -746,7 +754,7 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
         disc = __builtin_fmaf(a, -g0.w, -dot3(x, x));
         disc = c >= 0.0f ? __builtin_fminf(disc, hb * hb) : disc;
     }
-    if (behind | beyond | (disc < 0.0f))
+    if (culled | (disc < 0.0f))
         return kReject;
     const float sq = Math<kExact>::sqrt(disc);  // disc >= 0 here
     // the near root c/q (hb < 0, q = sq - hb), else the far root q/a, or -c/qn
@@ -849,7 +857,8 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.tb = kInf;
     tr.best = -1;
     for (int k = 0; k < A.n_big; ++k)
-        update_lex(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb), A.big_id[k], tr.tb, tr.best);
+        update_lex(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb, tr.tb * kCullScale),
+                   A.big_id[k], tr.tb, tr.best);
     if constexpr (kCount)
         cnt.spheres += A.n_big;
 #if PTG_BVH_WIDE
@@ -1134,15 +1143,18 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
     // 32-bit byte offsets on the uniform bases (saddr loads)
     const char *sph = (const char *)A.bvh_sph;
     const char *ids = (const char *)A.bvh_id;
+    float tbm = tb * kCullScale;
     for (int j = 0; j < cnt; ++j) {
         const unsigned off = (unsigned)(f + j) << 4;
-        const float t = root_lex<false, kExact>(*(const float4 *)(sph + off), float4{}, o, d, a, tb);
-        if (t <= tb)  // the scene index is read only for a candidate that wins or ties
+        const float t = root_lex<false, kExact>(*(const float4 *)(sph + off), float4{}, o, d, a, tb, tbm);
+        if (t <= tb) {  // the scene index is read only for a candidate that wins or ties
             update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
+            tbm = tb * kCullScale;
+        }
     }
 #else
     for (int j = 0; j < cnt; ++j) {
-        const float t = root_lex<false, kExact>(A.bvh_sph[f + j], float4{}, o, d, a, tb);
+        const float t = root_lex<false, kExact>(A.bvh_sph[f + j], float4{}, o, d, a, tb, tb * kCullScale);
         if (t <= tb)  // the scene index is read only for a candidate that wins or ties
             update_lex(t, A.bvh_id[f + j], tb, best);
     }
