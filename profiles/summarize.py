@@ -15,21 +15,28 @@ import shutil
 import sys
 
 
-def per_kernel(path, kernel_sub):
-    """Per counter, the value of the last dispatch of the timed kernel: the
-    render kernel without the counting template (render_kernel<false, ...>;
-    bench.py runs the counting kernel once, untimed), so neither it nor the
-    first, cold dispatch (up to 85 MB of extra reads measured) skews the
-    steady-state per-launch figures."""
+def per_kernel(path, kernel_sub, pick="last"):
+    """Per counter, the value of one dispatch of the timed kernel: the render
+    kernel without the counting template (render_kernel<false, ...>; bench.py
+    runs the counting kernel once, untimed).  pick="last": the last dispatch,
+    so the first, cold one (up to 85 MB of extra reads measured) does not skew
+    the steady-state per-launch figures.  pick="min": the smallest over the
+    timed kernel's dispatches -- for the HBM byte counters: the kernel's
+    traffic is deterministic (the image written once, the scene read), and
+    one pass (r04e) reported 205 MB of WRITE_SIZE for one of two identical
+    dispatches whose other read 24.3 MB, as every other pass did.  Also
+    returns every dispatch's value per counter."""
     rows = list(csv.DictReader(open(path)))
-    last = {}
+    per = collections.defaultdict(list)
     for r in rows:
         name = r["Kernel_Name"]
         if kernel_sub in name and (kernel_sub != "render_kernel" or "render_kernel<false" in name):
-            key, disp = r["Counter_Name"], int(r["Dispatch_Id"])
-            if key not in last or disp > last[key][0]:
-                last[key] = (disp, float(r["Counter_Value"]))
-    return {k: v[1] for k, v in last.items()}, rows
+            per[r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    if pick == "min":
+        val = {k: min(v for _, v in vs) for k, vs in per.items()}
+    else:
+        val = {k: max(vs)[1] for k, vs in per.items()}
+    return val, rows, {k: [v for _, v in sorted(vs)] for k, vs in per.items()}
 
 
 def main(src, tag, kernel_sub="render_kernel"):
@@ -42,15 +49,17 @@ def main(src, tag, kernel_sub="render_kernel"):
     render = [r for r in ks if kernel_sub in r["Name"] and "render_kernel<true" not in r["Name"]]
     calls = sum(int(r["Calls"]) for r in render)
     out["render_avg_ms"] = sum(float(r["TotalDurationNs"]) for r in render) / calls / 1e6
-    fetch, _ = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), kernel_sub)
-    write, _ = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), kernel_sub)
-    sq, rows = per_kernel(os.path.join(src, "sq", "run_counter_collection.csv"), kernel_sub)
+    fetch, _, fetch_all = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), kernel_sub, "min")
+    write, _, write_all = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), kernel_sub, "min")
+    sq, rows, _ = per_kernel(os.path.join(src, "sq", "run_counter_collection.csv"), kernel_sub)
     sq2p = os.path.join(src, "sq2", "run_counter_collection.csv")
     if os.path.exists(sq2p):
         sq.update(per_kernel(sq2p, kernel_sub)[0])
     fetch_b = fetch.get("FETCH_SIZE", 0.0) * 1024 * 2  # gfx950 FETCH_SIZE = 1/2 of wide-stream bytes
     write_b = write.get("WRITE_SIZE", 0.0) * 1024
-    out["hbm_bytes_per_launch"] = {"fetch_x2": fetch_b, "write": write_b, "total": fetch_b + write_b}
+    out["hbm_bytes_per_launch"] = {"fetch_x2": fetch_b, "write": write_b, "total": fetch_b + write_b,
+                                   "dispatches_KiB": {"FETCH_SIZE": fetch_all.get("FETCH_SIZE"),
+                                                      "WRITE_SIZE": write_all.get("WRITE_SIZE")}}
     out["sq"] = sq
     vgpr = [r for r in rows if kernel_sub in r["Kernel_Name"] and "render_kernel<true" not in r["Kernel_Name"]]
     if vgpr:
@@ -72,7 +81,7 @@ def main(src, tag, kernel_sub="render_kernel"):
             out["valu_insts_per_segment_wave_level"] = sq["SQ_INSTS_VALU"] * 64 / segs
     busyp = os.path.join(src, "busy", "run_counter_collection.csv")
     if os.path.exists(busyp):
-        bz, _ = per_kernel(busyp, kernel_sub)
+        bz = per_kernel(busyp, kernel_sub)[0]
         out["busy"] = bz
         grbm = bz.get("GRBM_GUI_ACTIVE", 0.0)
         if grbm > 0:
