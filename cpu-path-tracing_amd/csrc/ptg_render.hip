@@ -269,6 +269,10 @@ struct KArgs {
     // then the small spheres up to n
     int end_ax[3];
     int end_big;
+    // small records [end_big, end_out): spheres no ray can start inside
+    // (small_outside) -- the fast mode tests them for the outside case only
+    // (kSmallOut); then the other small records up to n
+    int end_out;
     // wall pairs (pair_walls): axis k's group starts with a pair when
     // pairs[k] = 1 -- its wall on the + side, then its wall on the - side; a
     // lane whose origin lies in [pair_lo[k], pair_hi[k]] tests only the wall
@@ -411,8 +415,11 @@ constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
 constexpr float kFarPlane = 1e30f;             // box mode: the room bound of an open side
 constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall skip test
 
-enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6 };
+enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6, kSmallOut = 7 };
 
+#ifndef PTG_SMALL_OUT
+#define PTG_SMALL_OUT 1  // fast mode: outside-only root for small spheres no ray starts inside (KArgs::small_out)
+#endif
 #ifndef PTG_BOX_WALL_LOOP
 #define PTG_BOX_WALL_LOOP 1  // box mode: extra walls one per lane per pass, with the exact cull (0: per-axis branches)
 #endif
@@ -479,7 +486,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             c = ee + g1.w;  // g1.w = -R^2
         }
         float disc;
-        if constexpr (kKind == kSmall) {
+        if constexpr (kKind == kSmall || kKind == kSmallOut) {
             // Lagrange's identity: hb^2 - a c = a R^2 - |e x d|^2.  hb^2 - a c
             // cancels to ~1e-3 relative for a sphere of radius r at distance
             // D >> r (two terms of size a D^2 for a difference of size a r^2);
@@ -495,7 +502,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #if PTG_SMALL_DISC_SKIP
         // a small sphere no lane's ray line meets cannot win: the wave skips
         // the root (exact: "win" below requires disc >= 0)
-        if constexpr (kKind == kSmall) {
+        if constexpr (kKind == kSmall || kKind == kSmallOut) {
             PTG_STAT(7);
             if (__ballot(!(disc < 0.0f)) == 0ull)
                 return;
@@ -507,9 +514,20 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         const bool neg = hb < 0.0f;
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
-        const bool near_lt = c < kEps * qq;
-        const float num = neg ? (near_lt ? qq : c) : -c;
-        const float den = (neg & near_lt) ? a : qq;
+        float num, den;
+        if constexpr (kKind == kSmallOut) {
+            // origin outside (c >= 0 up to the rounding of a hit point): the
+            // near root c/qq (hb < 0) or nothing (hb >= 0: -c/qq <= 0 fails
+            // the eps test); the far root qq/a is never needed -- an origin
+            // rounded just inside now fails "num < eps den" and the ray
+            // leaves, as in exact arithmetic
+            num = neg ? c : -c;
+            den = qq;
+        } else {
+            const bool near_lt = c < kEps * qq;
+            num = neg ? (near_lt ? qq : c) : -c;
+            den = (neg & near_lt) ? a : qq;
+        }
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
         const bool win = valid & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
@@ -693,6 +711,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     }
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
+#if PTG_SMALL_OUT
+    if constexpr (!kExact)
+        for (; i < A.end_out; ++i)
+            test(i, std::integral_constant<int, kSmallOut>{});
+#endif
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
     tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
@@ -2434,9 +2457,30 @@ void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::v
     A.box_mode = 1;
 }
 
+// A sphere no ray can start inside (KArgs::end_out).  A camera ray starts
+// outside every sphere whose centre is farther from the camera than its
+// radius plus the lens offset (<= 2 lens radii: camera_ray's rd * (s + t));
+// a ray reaches a surface point
+// only from outside every opaque sphere it has not hit before, and a diffuse
+// or mirror bounce leaves outward -- so, by induction, only dielectric
+// spheres are ever entered (up to the fp32 rounding of a hit point next to a
+// contact between two spheres, where the outside-only root lets the ray
+// leave, as in exact arithmetic).
+bool small_outside(const ptg_sphere &s, const ptg_camera *cam)
+{
+    double d2 = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        const double t = s.position[c] - cam->position[c];
+        d2 += t * t;
+    }
+    const double reach = s.radius + 4.0 * cam->lens_radius + 1e-6 * (1.0 + s.radius);
+    return PTG_SMALL_OUT && s.material != PTG_DIELECTRIC && d2 > reach * reach;
+}
+
 // Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z
 // (each axis group led by its wall pair, + wall first), then the other huge
-// spheres, then the small ones, each group otherwise in scene index order;
+// spheres, then the small ones (those no ray starts inside first, up to
+// end_out), each group otherwise in scene index order;
 // end_ax / end_big / pairs receive the group ends and pair flags.
 std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
                                const std::vector<GeoRec> &geo, KArgs &A)
@@ -2460,11 +2504,16 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam
         if (is_huge(s[i], cam) && axis[i] < 0)
             order.push_back(i);
     A.end_big = (int)order.size();
-    for (int i = 0; i < n; ++i)
-        if (!is_huge(s[i], cam))
-            order.push_back(i);
+    for (int pass = 0; pass < 2; ++pass) {  // spheres no ray starts inside first (end_out)
+        for (int i = 0; i < n; ++i)
+            if (!is_huge(s[i], cam) && small_outside(s[i], cam) == (pass == 0))
+                order.push_back(i);
+        if (pass == 0)
+            A.end_out = (int)order.size();
+    }
     return order;
 }
+
 
 // Records in scan order.  Axis-anchored records carry the signs in their
 // constants: g0.w = s R, g1.w = s 2R (the kernel reads e_k and d_k).
@@ -2842,6 +2891,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     }
     A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
     A.end_big = order.end_big;
+    A.end_out = order.end_out;
     if ((int)n_spheres > kLinearMax) {
         std::vector<char> huge(n_spheres);
         for (size_t i = 0; i < n_spheres; ++i)
