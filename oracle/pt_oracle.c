@@ -862,7 +862,9 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
     /* linear scan order (the kernel's record order, ptg_render.hip
      * prepare_scan_order): x-, y-, z-axis-anchored huge spheres (each axis
      * led by its wall pair, + wall first), the other huge spheres, the small
-     * ones; each group otherwise in index order */
+     * ones -- those no ray starts inside first (ptg_render.hip small_outside:
+     * not dielectric, centre farther from the camera than radius + 4 lens
+     * radii + 1e-6 (1 + radius)); each group otherwise in index order */
     if (n <= LINEAR_MAX_PREP) {
         pair_walls_B(s, n, cam, &box, out);
         box_mode_B(s, n, cam, &box, out);
@@ -881,9 +883,20 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         for (int i = 0; i < n; ++i)
             if (out[i].big && out[i].axis < 0)
                 out[j++].visit = i;
-        for (int i = 0; i < n; ++i)
-            if (!out[i].big)
-                out[j++].visit = i;
+        for (int pass = 0; pass < 2; ++pass)
+            for (int i = 0; i < n; ++i) {
+                if (out[i].big)
+                    continue;
+                double d2 = 0.0;
+                for (int c = 0; c < 3; ++c) {
+                    const double t = s[i].position[c] - cam->position[c];
+                    d2 += t * t;
+                }
+                const double reach = s[i].radius + 4.0 * cam->lens_radius + 1e-6 * (1.0 + s[i].radius);
+                const int outside = s[i].material != 2 /* dielectric */ && d2 > reach * reach;
+                if (outside == (pass == 0))
+                    out[j++].visit = i;
+            }
     } else {
         for (int i = 0; i < n; ++i)
             out[i].visit = i;
