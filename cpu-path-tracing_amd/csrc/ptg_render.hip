@@ -270,9 +270,10 @@ struct KArgs {
     int end_ax[3];
     int end_big;
     // small records [end_big, end_out): spheres no ray can start inside
-    // (small_outside) -- the fast mode tests them for the outside case only
+    // (outside_only) -- the fast mode tests them for the outside case only
     // (kSmallOut); then the other small records up to n
     int end_out;
+    int box_walls_out;  // box mode's walls: no ray starts inside any (outside_only); else the fast mode scans generically
     // wall pairs (pair_walls): axis k's group starts with a pair when
     // pairs[k] = 1 -- its wall on the + side, then its wall on the - side; a
     // lane whose origin lies in [pair_lo[k], pair_hi[k]] tests only the wall
@@ -415,7 +416,7 @@ constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
 constexpr float kFarPlane = 1e30f;             // box mode: the room bound of an open side
 constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall skip test
 
-enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6, kSmallOut = 7 };
+enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6, kSmallOut = 7, kAxAnyOut = 8 };
 
 #ifndef PTG_SMALL_OUT
 #define PTG_SMALL_OUT 1  // fast mode: outside-only root for small spheres no ray starts inside (KArgs::small_out)
@@ -448,7 +449,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         if constexpr (kKind <= kAxZ) {  // huge sphere anchored on axis k: g0.w = +-R, g1.w = +-2R
             hb = __builtin_fmaf(g0.w, comp(d, kKind), ed);
             c = __builtin_fmaf(g1.w, comp(e, kKind), ee);
-        } else if constexpr (kKind == kAxAny) {
+        } else if constexpr (kKind == kAxAny || kKind == kAxAnyOut) {
             // the same, for the wall the ray moves toward on a per-lane axis
             // k: g0.w d_k = -R |d_k| = -|g0.w| vn and g1.w e_k = 2R u = |g1.w| un
             // (un: the plane distance numerator, the same subtraction as e_k
@@ -515,13 +516,13 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
         float num, den;
-        if constexpr (kKind == kSmallOut) {
+        if constexpr (kKind == kSmallOut || kKind == kAxAnyOut) {
             // origin outside (c >= 0 up to the rounding of a hit point): the
             // near root c/qq (hb < 0) or nothing (hb >= 0: -c/qq <= 0 fails
-            // the eps test); the far root qq/a is never needed -- an origin
-            // rounded just inside now fails "num < eps den" and the ray
-            // leaves, as in exact arithmetic
-            num = neg ? c : -c;
+            // the eps test; `win` below requires hb < 0); the far root qq/a
+            // is never needed -- an origin rounded just inside fails "num <
+            // eps den" and the ray leaves, as in exact arithmetic
+            num = c;
             den = qq;
         } else {
             const bool near_lt = c < kEps * qq;
@@ -530,7 +531,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         }
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
-        const bool win = valid & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
+        bool win = valid & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
+        if constexpr (kKind == kSmallOut || kKind == kAxAnyOut)
+            win = win & neg;
         bn = win ? num : bn;
         bq = win ? den : bq;
         best = win ? r : best;
@@ -606,7 +609,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls + 2 * kn) +
                                                       (comp(d, kn) >= 0.0f ? 0 : 4));
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
-        test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, kAxAny>{}, un, vn, in >= 0);
+        // (fast mode: box mode runs only when no ray starts inside a wall --
+        // KArgs::box_walls_out -- so the outside-only roots apply)
+        test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, (PTG_SMALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{},
+                 un, vn, in >= 0);
         const float bqm = bq * kPlaneMargin;
         bool need[3];
         for (int k = 0; k < 3; ++k) {
@@ -2405,10 +2411,34 @@ void pair_walls(const ptg_sphere *s, int n, const std::vector<int> &axis, const 
 // records' anchor coordinate), and extends the pair bounds to single walls
 // (margin as pair_walls) and open sides (+-kFarPlane).  The oracle's prep_B
 // makes the same choice.
+// A sphere no ray can start inside (KArgs::end_out, box_walls_out).  A camera ray starts
+// outside every sphere whose centre is farther from the camera than its
+// radius plus the lens offset (< 2 lens radii: camera_ray's rd * (s + t));
+// a ray reaches a surface point
+// only from outside every opaque sphere it has not hit before, and a diffuse
+// or mirror bounce leaves outward -- so, by induction, only dielectric
+// spheres are ever entered (up to the fp32 rounding of a hit point next to a
+// contact between two spheres, where the outside-only root lets the ray
+// leave, as in exact arithmetic).
+bool outside_only(const ptg_sphere &s, const ptg_camera *cam)
+{
+    double d2 = 0.0, p2 = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        const double t = s.position[c] - cam->position[c];
+        d2 += t * t;
+        p2 += cam->position[c] * cam->position[c];
+    }
+    // margins: the lens bound's, the fp32 rounding of a camera origin, the
+    // double rounding of d2
+    const double reach = s.radius + 2.0001 * cam->lens_radius + 1e-6 * (1.0 + std::sqrt(p2)) + 1e-9 * s.radius;
+    return PTG_SMALL_OUT && s.material != PTG_DIELECTRIC && d2 > reach * reach;
+}
+
 void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
                  const std::vector<GeoRec> &geo, const std::vector<int> &order, KArgs &A)
 {
     A.box_mode = 0;
+    A.box_walls_out = 0;
     int cnt[3] = {0, 0, 0}, general = 0;
     for (int i = 0; i < n; ++i) {
         if (!is_huge(s[i], cam))
@@ -2455,27 +2485,12 @@ void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::v
             A.pair_lo[k] = -kFarPlane;
     }
     A.box_mode = 1;
+    A.box_walls_out = 1;
+    for (int i = 0; i < n; ++i)
+        if (is_huge(s[i], cam) && axis[i] >= 0 && !outside_only(s[i], cam))
+            A.box_walls_out = 0;
 }
 
-// A sphere no ray can start inside (KArgs::end_out).  A camera ray starts
-// outside every sphere whose centre is farther from the camera than its
-// radius plus the lens offset (<= 2 lens radii: camera_ray's rd * (s + t));
-// a ray reaches a surface point
-// only from outside every opaque sphere it has not hit before, and a diffuse
-// or mirror bounce leaves outward -- so, by induction, only dielectric
-// spheres are ever entered (up to the fp32 rounding of a hit point next to a
-// contact between two spheres, where the outside-only root lets the ray
-// leave, as in exact arithmetic).
-bool small_outside(const ptg_sphere &s, const ptg_camera *cam)
-{
-    double d2 = 0.0;
-    for (int c = 0; c < 3; ++c) {
-        const double t = s.position[c] - cam->position[c];
-        d2 += t * t;
-    }
-    const double reach = s.radius + 4.0 * cam->lens_radius + 1e-6 * (1.0 + s.radius);
-    return PTG_SMALL_OUT && s.material != PTG_DIELECTRIC && d2 > reach * reach;
-}
 
 // Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z
 // (each axis group led by its wall pair, + wall first), then the other huge
@@ -2506,7 +2521,7 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam
     A.end_big = (int)order.size();
     for (int pass = 0; pass < 2; ++pass) {  // spheres no ray starts inside first (end_out)
         for (int i = 0; i < n; ++i)
-            if (!is_huge(s[i], cam) && small_outside(s[i], cam) == (pass == 0))
+            if (!is_huge(s[i], cam) && outside_only(s[i], cam) == (pass == 0))
                 order.push_back(i);
         if (pass == 0)
             A.end_out = (int)order.size();
@@ -2584,6 +2599,8 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.count_tests = (p->flags & PTG_FLAG_COUNT_TESTS) != 0;
     A.count_nonfinite = (p->flags & PTG_FLAG_COUNT_NONFINITE) != 0;
     A.exact_math = (p->flags & PTG_FLAG_EXACT_MATH) != 0;
+    if (PTG_SMALL_OUT && !A.exact_math && !A.box_walls_out)
+        A.box_mode = 0;  // the fast mode's box-mode wall test assumes rays outside the walls
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
@@ -2892,6 +2909,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
     A.end_big = order.end_big;
     A.end_out = order.end_out;
+    A.box_walls_out = order.box_walls_out;
     if ((int)n_spheres > kLinearMax) {
         std::vector<char> huge(n_spheres);
         for (size_t i = 0; i < n_spheres; ++i)
