@@ -862,9 +862,7 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
     /* linear scan order (the kernel's record order, ptg_render.hip
      * prepare_scan_order): x-, y-, z-axis-anchored huge spheres (each axis
      * led by its wall pair, + wall first), the other huge spheres, the small
-     * ones -- those no ray starts inside first (ptg_render.hip small_outside:
-     * not dielectric, centre farther from the camera than radius + 2.0001
-     * lens radii + 1e-6 (1 + |camera|) + 1e-9 radius); each group otherwise in index order */
+     * ones; each group otherwise in index order */
     if (n <= LINEAR_MAX_PREP) {
         pair_walls_B(s, n, cam, &box, out);
         box_mode_B(s, n, cam, &box, out);
@@ -883,22 +881,9 @@ static void prep_B(const po_sphere *s, int n, const po_camera *cam, sphB *out, c
         for (int i = 0; i < n; ++i)
             if (out[i].big && out[i].axis < 0)
                 out[j++].visit = i;
-        for (int pass = 0; pass < 2; ++pass)
-            for (int i = 0; i < n; ++i) {
-                if (out[i].big)
-                    continue;
-                double d2 = 0.0, p2 = 0.0;
-                for (int c = 0; c < 3; ++c) {
-                    const double t = s[i].position[c] - cam->position[c];
-                    d2 += t * t;
-                    p2 += cam->position[c] * cam->position[c];
-                }
-                const double reach =
-                    s[i].radius + 2.0001 * cam->lens_radius + 1e-6 * (1.0 + sqrt(p2)) + 1e-9 * s[i].radius;
-                const int outside = s[i].material != 2 /* dielectric */ && d2 > reach * reach;
-                if (outside == (pass == 0))
-                    out[j++].visit = i;
-            }
+        for (int i = 0; i < n; ++i)
+            if (!out[i].big)
+                out[j++].visit = i;
     } else {
         for (int i = 0; i < n; ++i)
             out[i].visit = i;
