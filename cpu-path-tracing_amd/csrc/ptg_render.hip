@@ -269,10 +269,6 @@ struct KArgs {
     // then the small spheres up to n
     int end_ax[3];
     int end_big;
-    // small records [end_big, end_out): spheres no ray can start inside
-    // (outside_only) -- the fast mode tests them for the outside case only
-    // (kSmallOut); then the other small records up to n
-    int end_out;
     int box_walls_out;  // box mode's walls: no ray starts inside any (outside_only); else the fast mode scans generically
     // wall pairs (pair_walls): axis k's group starts with a pair when
     // pairs[k] = 1 -- its wall on the + side, then its wall on the - side; a
@@ -416,10 +412,10 @@ constexpr float kCullMargin = 0x1.00001p+0f;  // 1 + 2^-20 (BVH leaf test)
 constexpr float kFarPlane = 1e30f;             // box mode: the room bound of an open side
 constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall skip test
 
-enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6, kSmallOut = 7, kAxAnyOut = 8 };
+enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6, kAxAnyOut = 7 };
 
-#ifndef PTG_SMALL_OUT
-#define PTG_SMALL_OUT 1  // fast mode: outside-only root for small spheres no ray starts inside (KArgs::small_out)
+#ifndef PTG_WALL_OUT
+#define PTG_WALL_OUT 1  // fast mode, box mode: the nearest wall's outside-only root (KArgs::box_walls_out)
 #endif
 #ifndef PTG_BOX_WALL_LOOP
 #define PTG_BOX_WALL_LOOP 1  // box mode: extra walls one per lane per pass, with the exact cull (0: per-axis branches)
@@ -487,7 +483,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             c = ee + g1.w;  // g1.w = -R^2
         }
         float disc;
-        if constexpr (kKind == kSmall || kKind == kSmallOut) {
+        if constexpr (kKind == kSmall) {
             // Lagrange's identity: hb^2 - a c = a R^2 - |e x d|^2.  hb^2 - a c
             // cancels to ~1e-3 relative for a sphere of radius r at distance
             // D >> r (two terms of size a D^2 for a difference of size a r^2);
@@ -503,7 +499,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #if PTG_SMALL_DISC_SKIP
         // a small sphere no lane's ray line meets cannot win: the wave skips
         // the root (exact: "win" below requires disc >= 0)
-        if constexpr (kKind == kSmall || kKind == kSmallOut) {
+        if constexpr (kKind == kSmall) {
             PTG_STAT(7);
             if (__ballot(!(disc < 0.0f)) == 0ull)
                 return;
@@ -516,12 +512,16 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // sq - hb (hb < 0) and hb + sq (hb >= 0) are the same IEEE add
         const float qq = sq + __builtin_fabsf(hb);
         float num, den;
-        if constexpr (kKind == kSmallOut || kKind == kAxAnyOut) {
-            // origin outside (c >= 0 up to the rounding of a hit point): the
-            // near root c/qq (hb < 0) or nothing (hb >= 0: -c/qq <= 0 fails
-            // the eps test; `win` below requires hb < 0); the far root qq/a
-            // is never needed -- an origin rounded just inside fails "num <
-            // eps den" and the ray leaves, as in exact arithmetic
+        if constexpr (kKind == kAxAnyOut) {
+            // a box wall, origin outside it (box_walls_out): the near root
+            // c/qq (hb < 0) or nothing (hb >= 0: -c/qq <= 0 fails the eps
+            // test; `win` below requires hb < 0).  The far root qq/a -- the
+            // wall sphere's other side, ~2R away -- is dropped: the
+            // reference takes it only for an origin within eps of the wall
+            // moving toward it (a surface touching the wall); the bench
+            // frame's quality rows are unchanged up to single roundings
+            // (profiles/r04_kernel_ab.txt 13).  The same for the small
+            // spheres moved paths there (item 12): not done.
             num = c;
             den = qq;
         } else {
@@ -532,7 +532,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
         bool win = valid & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
-        if constexpr (kKind == kSmallOut || kKind == kAxAnyOut)
+        if constexpr (kKind == kAxAnyOut)
             win = win & neg;
         bn = win ? num : bn;
         bq = win ? den : bq;
@@ -611,7 +611,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
-        test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, (PTG_SMALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{},
+        test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{},
                  un, vn, in >= 0);
         const float bqm = bq * kPlaneMargin;
         bool need[3];
@@ -717,11 +717,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     }
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
-#if PTG_SMALL_OUT
-    if constexpr (!kExact)
-        for (; i < A.end_out; ++i)
-            test(i, std::integral_constant<int, kSmallOut>{});
-#endif
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
     tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
@@ -2411,7 +2406,7 @@ void pair_walls(const ptg_sphere *s, int n, const std::vector<int> &axis, const 
 // records' anchor coordinate), and extends the pair bounds to single walls
 // (margin as pair_walls) and open sides (+-kFarPlane).  The oracle's prep_B
 // makes the same choice.
-// A sphere no ray can start inside (KArgs::end_out, box_walls_out).  A camera ray starts
+// A sphere no ray can start inside (KArgs::box_walls_out).  A camera ray starts
 // outside every sphere whose centre is farther from the camera than its
 // radius plus the lens offset (< 2 lens radii: camera_ray's rd * (s + t));
 // a ray reaches a surface point
@@ -2431,7 +2426,7 @@ bool outside_only(const ptg_sphere &s, const ptg_camera *cam)
     // margins: the lens bound's, the fp32 rounding of a camera origin, the
     // double rounding of d2
     const double reach = s.radius + 2.0001 * cam->lens_radius + 1e-6 * (1.0 + std::sqrt(p2)) + 1e-9 * s.radius;
-    return PTG_SMALL_OUT && s.material != PTG_DIELECTRIC && d2 > reach * reach;
+    return PTG_WALL_OUT && s.material != PTG_DIELECTRIC && d2 > reach * reach;
 }
 
 void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
@@ -2494,8 +2489,7 @@ void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::v
 
 // Linear scenes: scan order (scene_scan) -- huge spheres anchored on x, y, z
 // (each axis group led by its wall pair, + wall first), then the other huge
-// spheres, then the small ones (those no ray starts inside first, up to
-// end_out), each group otherwise in scene index order;
+// spheres, then the small ones, each group otherwise in scene index order;
 // end_ax / end_big / pairs receive the group ends and pair flags.
 std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
                                const std::vector<GeoRec> &geo, KArgs &A)
@@ -2519,13 +2513,9 @@ std::vector<int> scan_order_of(const ptg_sphere *s, int n, const ptg_camera *cam
         if (is_huge(s[i], cam) && axis[i] < 0)
             order.push_back(i);
     A.end_big = (int)order.size();
-    for (int pass = 0; pass < 2; ++pass) {  // spheres no ray starts inside first (end_out)
-        for (int i = 0; i < n; ++i)
-            if (!is_huge(s[i], cam) && outside_only(s[i], cam) == (pass == 0))
-                order.push_back(i);
-        if (pass == 0)
-            A.end_out = (int)order.size();
-    }
+    for (int i = 0; i < n; ++i)
+        if (!is_huge(s[i], cam))
+            order.push_back(i);
     return order;
 }
 
@@ -2599,7 +2589,7 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.count_tests = (p->flags & PTG_FLAG_COUNT_TESTS) != 0;
     A.count_nonfinite = (p->flags & PTG_FLAG_COUNT_NONFINITE) != 0;
     A.exact_math = (p->flags & PTG_FLAG_EXACT_MATH) != 0;
-    if (PTG_SMALL_OUT && !A.exact_math && !A.box_walls_out)
+    if (PTG_WALL_OUT && !A.exact_math && !A.box_walls_out)
         A.box_mode = 0;  // the fast mode's box-mode wall test assumes rays outside the walls
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
@@ -2908,7 +2898,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     }
     A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
     A.end_big = order.end_big;
-    A.end_out = order.end_out;
     A.box_walls_out = order.box_walls_out;
     if ((int)n_spheres > kLinearMax) {
         std::vector<char> huge(n_spheres);
