@@ -414,6 +414,9 @@ constexpr float kPlaneMargin = 0x1.ffep-1f;    // 1 - 2^-12: box mode's wall ski
 
 enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAxSel = 6, kAxAnyOut = 7 };
 
+#ifndef PTG_UNIT_ROUNDS
+#define PTG_UNIT_ROUNDS 2  // linear scenes below the split-tail size: work units for this many rounds of wave slots (2 beats 4 by 5 %, 12 by 12 % on C1)
+#endif
 #ifndef PTG_WALL_OUT
 #define PTG_WALL_OUT 1  // fast mode, box mode: the nearest wall's outside-only root (KArgs::box_walls_out)
 #endif
@@ -2614,7 +2617,11 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     if (tail_ok) {
         chunk = nsamp;
     } else if (chunk <= 0) {
-        const long long target = ctx->n > kLinearMax ? PTG_BVH_UNIT_MULT * 98304 : 98304;
+        // (linear scenes: PTG_UNIT_ROUNDS rounds of the device's wave slots --
+        // C1's 7,500 pixel groups in 6-sample units, 22,500 units: 12 %
+        // faster than ~96k units of 2 samples, whose per-unit setup weighed)
+        const long long target =
+            ctx->n > kLinearMax ? PTG_BVH_UNIT_MULT * 98304 : (long long)PTG_UNIT_ROUNDS * ctx->wave_slots;
         long long want = (target + groups - 1) / groups;
         long long nch = want < 1 ? 1 : (want > nsamp ? nsamp : want);
         chunk = nch > 0 ? (int)((nsamp + nch - 1) / nch) : 1;
