@@ -2,17 +2,20 @@
 """Benchmark: Mray-samples/s of the MI355X render loop (BASELINE.json metric).
 
 One step = one full frame of the workload rendered by the HIP megakernel,
-scene and output already resident in HBM.  Workload (--workload auto): on one
-GPU the metric's frame, box_scene.hpp at 1920x1080, 1024 spp (256 samples per
-sub-pixel); with N > 1 ranks (torchrun, one process per GPU) BASELINE.json
-configs[3] = C4, box_scene at 3840x2160, 4096 spp, tile-sharded by
-interleaved row bands, the step including the single gather (RCCL over xGMI)
-to rank 0 and the un-shard.  value = whole-frame samples / max-over-ranks time
-(strong scaling: the frame is fixed for a given N).  At N > 1 rank 0 first
-renders the same frame alone (untimed for `value`) and the line carries
-t1_ms and efficiency = T1 / (N * T_N) of this run, so the scaling line is
-self-contained (the N = 1 default line is the metric's 1080p frame).
---workload c1..c5 / bench pick one config for every N.
+scene and output already resident in HBM.  Workload: the metric's frame,
+box_scene.hpp at 1920x1080, 1024 spp (256 samples per sub-pixel), for EVERY
+N -- so the N = 1, 2, 4, 8 lines of a scaling run measure the same frame.
+With N > 1 GPUs the frame is tile-sharded by interleaved row bands, the step
+including the single gather (RCCL over xGMI) to rank 0 and the un-shard.
+value = whole-frame samples / max-over-ranks time (strong scaling: the frame
+is fixed).  At N > 1 rank 0 first renders the same frame alone (untimed for
+`value`) and the line carries t1_ms and efficiency = T1 / (N * T_N) of this
+run, so the scaling line is self-contained.  --workload c1..c5 picks another
+BASELINE.json config (C4: box 3840x2160x4096spp); the line's metric string
+then names the frame actually rendered.  Every N > 1 line carries what the
+RCCL group actually was -- rccl_ranks (ncclCommCount of every communicator),
+the devices and their PCI bus ids -- and bench.py exits 3 instead of printing
+a line when fewer than N ranks or distinct devices took part.
 
 Launch modes (resolve_launch):
   * WORLD_SIZE unset, --gpus 1           one GPU.
@@ -28,6 +31,9 @@ Launch modes (resolve_launch):
   * WORLD_SIZE set and != --gpus         an error (exit 2): the line would
                                          otherwise claim a GPU count it did not
                                          measure.
+  * --launch inprocess                   the one-process ptg_multi path at any N,
+                                         also N = 1 (a one-rank RCCL group: the
+                                         1-GPU box rehearsal of that path).
 PTG_REHEARSAL=1 runs either N > 1 mode on one GPU (N shards on device 0; gloo
 for torchrun) -- a 1-GPU box rehearsal of the sharded path, labelled as such.
 Efficiency = T1 / (N * T_N) with T1 and T_N timed the same way: wall clock
@@ -39,7 +45,13 @@ Also reported:
                   per launch (S_bar*(23*N_spheres + 100) + 60 per sample,
                   SURVEY.md 8(d), S_bar measured by the kernel's own segment
                   counter) / its average launch time from HIP events on the
-                  launch stream; peak 157.3 TFLOP/s (MI355X fp32 vector).
+                  launch stream; peak 157.3 TFLOP/s (MI355X fp32 vector, the
+                  packed rate) -> frac, and 78.6 TFLOP/s (the non-packed
+                  issue rate: the kernel is built without v_pk_*_f32, which on
+                  gfx950 cost two plain issue slots, MI355X_MICROARCH.md:491)
+                  -> frac_nonpacked; valu_fp32_share = FP32 add/mul/fma/trans
+                  instructions / all VALU instructions of the committed
+                  rocprofv3 profile of the workload.
   cpu_baseline -- the REFERENCE's own per-pixel code (src/main.cpp:27-197
                   compiled with its `pt` library into oracle/_ref/libref_main.so,
                   kind "reference") in an OpenMP row loop on the host's cores,
@@ -69,10 +81,14 @@ import torch.distributed as dist  # noqa: E402
 import ptgpu  # noqa: E402
 
 METRIC = "Mray-samples/sec at 1920×1080×1024spp; per-pixel RMSE vs CPU ref"
-PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate, packed
+# the non-packed FP32 VALU rate (256 CUs x 4 SIMDs x 32 lanes x 2 FLOP x 2.4
+# GHz): what a kernel without v_pk_*_f32 can issue at most
+PEAK_FP32_NONPACKED_TFLOPS = 78.6
 
 
 # BASELINE.json configs (C1..C5) plus the metric's own frame
+# (the default workload at every N)
 WORKLOADS = {
     "bench": ("box", 1920, 1080, 1024),       # the metric: box_scene at 1920x1080x1024spp on one MI355X
     "c1": ("simple", 400, 300, 64),
@@ -262,8 +278,11 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto",
-                    help="BASELINE.json config (auto: the metric's box 1920x1080x1024spp frame on one GPU, "
-                         "C4's box 3840x2160x4096spp frame when sharded over N > 1 GPUs)")
+                    help="BASELINE.json config (auto = bench: the metric's box 1920x1080x1024spp frame, at every N; "
+                         "c4: box 3840x2160x4096spp)")
+    ap.add_argument("--launch", choices=["auto", "inprocess"], default="auto",
+                    help="inprocess: the one-process ptg_multi path (RCCL communicators from ncclCommInitAll) "
+                         "even at --gpus 1")
     ap.add_argument("--scene", default=None, help="overrides the workload's scene")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
@@ -288,7 +307,11 @@ def parse_args(argv=None):
 
 
 def frame_config(args, world):
-    wl = args.workload if args.workload != "auto" else ("bench" if world == 1 else "c4")
+    """The frame for every N: the metric's (bench) unless --workload / the
+    size flags say otherwise (`world` does not change it: a scaling run's
+    lines compare one frame)."""
+    del world
+    wl = args.workload if args.workload != "auto" else "bench"
     wscene, wW, wH, wspp = WORKLOADS[wl]
     scene = args.scene or wscene
     nsub = 2  # main.cpp:202
@@ -297,6 +320,68 @@ def frame_config(args, world):
     spp = samps * nsub * nsub
     wl_name = wl if (scene, W, H, spp) == WORKLOADS[wl] else "custom"
     return wl_name, scene, W, H, samps, nsub, spp
+
+
+def metric_of(scene, W, H, spp):
+    """BASELINE.json's metric string when the frame is the metric's own
+    (box 1920x1080x1024spp), else the same metric named for the frame
+    actually rendered."""
+    if (scene, W, H, spp) == WORKLOADS["bench"]:
+        return METRIC
+    return f"Mray-samples/sec at {W}×{H}×{spp}spp ({scene}); per-pixel RMSE vs CPU ref"
+
+
+def check_group(n, ranks, devices, bus_ids, rehearsal):
+    """Problems with an N-GPU measurement's RCCL group (empty: none): every
+    communicator has N ranks, the N ranks run on N distinct devices with N
+    distinct PCI bus ids.  A rehearsal (N shards on one GPU) is exempt; None
+    entries (not determinable) are not counted as evidence either way."""
+    if rehearsal or n <= 1:
+        return []
+    bad = []
+    known = [r for r in ranks if r is not None]
+    if any(r != n for r in known):
+        bad.append(f"RCCL communicators of {sorted(set(known))} ranks, not {n}")
+    if len(set(devices)) != n:
+        bad.append(f"{len(set(devices))} distinct devices for {n} ranks: {devices}")
+    kb = [b for b in bus_ids if b]
+    if len(kb) == n and len(set(kb)) != n:
+        bad.append(f"{len(set(kb))} distinct PCI bus ids for {n} ranks: {bus_ids}")
+    return bad
+
+
+def torch_rccl_info(local):
+    """(ncclCommCount, ncclCommCuDevice, ncclCommUserRank) of the default
+    process group's RCCL communicator on this rank's device, read with the
+    RCCL library torch itself loaded (torch/lib/librccl.so, whose struct the
+    handle belongs to); (None, None, None, reason) when not determinable."""
+    import ctypes as C
+    try:
+        pg = dist.distributed_c10d._get_default_group()
+        backend = pg._get_backend(torch.device("cuda", local))
+        ptr = int(backend._comm_ptr())
+        if not ptr:
+            return None, None, None, "no communicator"
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        L = C.CDLL(path if os.path.exists(path) else "librccl.so")
+        out = []
+        for fn in ("ncclCommCount", "ncclCommCuDevice", "ncclCommUserRank"):
+            v = C.c_int(-1)
+            rc = getattr(L, fn)(C.c_void_p(ptr), C.byref(v))
+            if rc != 0:
+                return None, None, None, f"{fn} returned {rc}"
+            out.append(int(v.value))
+        return out[0], out[1], out[2], None
+    except Exception as e:  # noqa: BLE001 -- reported in the line, not fatal
+        return None, None, None, f"{type(e).__name__}: {e}"
+
+
+def bus_id_of(device):
+    """PCI bus id of a visible device (hipDeviceGetPCIBusId via the C ABI)."""
+    try:
+        return ptgpu.pci_bus_id(device)
+    except Exception as e:  # noqa: BLE001
+        return f"unknown ({e})"
 
 
 def arith_flags(args):
@@ -324,6 +409,15 @@ def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms
         "bound": "valu", "achieved": round(achieved, 3) if achieved else None,
         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
+        # against the non-packed FP32 issue rate (the kernel is built without
+        # v_pk_*_f32: on gfx950 a packed op costs two plain issue slots,
+        # MI355X_MICROARCH.md:491, and the pair moves made it 7.8 % slower)
+        "peak_nonpacked": PEAK_FP32_NONPACKED_TFLOPS,
+        "frac_nonpacked": round(achieved / PEAK_FP32_NONPACKED_TFLOPS, 4) if achieved else None,
+        # FP32 add/mul/fma/trans share of the VALU instructions the profile
+        # counted (the rest: compares, selects, moves, integer, converts --
+        # real issue slots the FLOP model does not count)
+        "valu_fp32_share": pmc.get("valu_fp32_share"),
         "traffic": pmc.get("hbm_bytes_per_launch"),
         "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
         "segments_per_sample": round(s_bar, 4),
@@ -345,7 +439,7 @@ def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms
 def base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, parallelism):
     value = W * H * spp * args.steps / elapsed / 1e6
     return value, {
-        "metric": METRIC,
+        "metric": metric_of(scene, W, H, spp),
         "value": round(value, 2),
         "unit": "Mray-samples/s",
         "n_gpus": world,
@@ -365,11 +459,12 @@ def base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapse
 
 
 def run_inprocess(args):
-    """--gpus N > 1 without a launcher: one process, ptg_multi over GPUs
-    0..N-1 (the scene on every device, ONE ncclGather per frame over xGMI,
-    the un-shard on GPU 0; csrc/ptg_multi.cpp).  A step is one frame kept in
-    HBM.  T1 is the same frame through a one-device ptg_multi (render, slab
-    copy, un-shard), timed the same way."""
+    """--gpus N > 1 without a launcher (or --launch inprocess): one process,
+    ptg_multi over GPUs 0..N-1 (the scene on every device, ONE ncclGather per
+    frame over xGMI, the un-shard on GPU 0; csrc/ptg_multi.cpp).  A step is
+    one frame kept in HBM.  T1 is the same frame through a one-device
+    ptg_multi (render, slab copy -- a device copy, not RCCL -- un-shard),
+    timed the same way."""
     n = args.gpus
     rehearsal = os.environ.get("PTG_REHEARSAL") == "1"
     visible = torch.cuda.device_count()
@@ -388,6 +483,18 @@ def run_inprocess(args):
     cparams = ptgpu.make_params(W, H, samps, nsub, ptgpu.DEFAULT_SEED, args.band_rows, 0, 1, args.chunk,
                                 flags=flags | ptgpu.FLAG_COUNT_TESTS)
     mc = ptgpu.MultiContext(scn, cam, list(range(n)), local_shards=n if rehearsal else 0)
+    # what the group is: ncclCommCount / ncclCommCuDevice of every communicator
+    info = mc.comm_info()
+    ranks = [r if r > 0 else None for r, _, _ in info]
+    devs = [d for _, d, _ in info]
+    bus = [bus_id_of(d) for d in devs]
+    bad = check_group(n, ranks if not rehearsal else [], devs, bus, rehearsal)
+    if not rehearsal and any(r is None for r in ranks):
+        bad.append(f"shards without an RCCL communicator: {info}")
+    if bad:
+        mc.close()
+        log("error: the N-GPU group is not what the line would report: " + "; ".join(bad))
+        sys.exit(3)
     counters = mc.frame_device(cparams, counters=True)  # S_bar from the kernels' own counters (untimed)
     seg_total, sph_total, box_total = (int(v) for v in counters[:3])
     for _ in range(max(0, args.warmup - 1)):
@@ -423,18 +530,30 @@ def run_inprocess(args):
 
     frame_samples = W * H * spp
     pmc = load_pmc(f"{scene} {W}x{H} {spp}spp")
-    my_samples = frame_samples / n  # equal shards: N divides the bands
-    s_bar, roof = roofline(frame_samples, seg_total, sph_total, box_total, my_samples, float(kern_dev.mean()),
+    # each device's own share (band rows are not always split evenly): the
+    # roofline's `achieved` is the slowest device's samples over its own
+    # kernel time
+    dev_samples = [int((ptgpu.slab_to_image_rows(H, args.band_rows, k, n) >= 0).sum()) * W * spp for k in range(n)]
+    slow = int(np.argmax(kern_dev))
+    s_bar, roof = roofline(frame_samples, seg_total, sph_total, box_total, dev_samples[slow], float(kern_dev[slow]),
                            n_sph, pmc)
     par = (f"tile-sharded row bands x{n}, one process (ptg_multi: ncclCommInitAll + ONE ncclGather per frame)"
            + (f" -- REHEARSAL: {n} shards on one GPU, gathered by device copies" if rehearsal else ""))
     value, out = base_line(args, n, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, par)
     out["segments_per_s"] = round(value * 1e6 * s_bar, 1)
     out["roofline"] = roof
-    out["roofline"]["note"] = "achieved: one GPU's kernel (mean over the N devices' HIP-event render times)"
+    out["roofline"]["note"] = (f"achieved: the slowest device's kernel (device {devs[slow]}: its {dev_samples[slow]} "
+                               f"samples over its HIP-event render time)")
     out["cpu_baseline"] = None
     out["launch"] = "inprocess"
+    out["rccl_ranks"] = None if rehearsal else ranks
+    out["devices"] = [{"shard": k, "device": d, "pci_bus_id": b, "rccl_user_rank": u}
+                      for k, ((_, d, u), b) in enumerate(zip(info, bus))]
+    out["group_check"] = ("rehearsal: local shards, no RCCL communicator" if rehearsal else
+                          f"ok: {n} RCCL ranks per communicator on {len(set(devs))} distinct devices / "
+                          f"{len(set(bus))} PCI bus ids")
     out["per_rank"] = {"render_ms": [round(float(x), 3) for x in kern_dev],
+                       "samples": dev_samples,
                        "frame_ms_root": round(float(np.mean(frame_ms)), 3),
                        "note": "HIP events: each device's render; frame_ms_root = GPU 0's render start to the "
                                "end of the gather + un-shard"}
@@ -442,8 +561,8 @@ def run_inprocess(args):
         tn_wall = elapsed / args.steps * 1e3
         tn_kern = float(render_ms.max(1).mean())  # the slowest shard per frame
         out["t1_ms"] = t1["wall_ms"]
-        out["t1"] = dict(t1, note="the same frame on GPU 0 alone through a one-device ptg_multi, wall clock per "
-                                  "frame like ms_per_step")
+        out["t1"] = dict(t1, note="the same frame on GPU 0 alone through a one-device ptg_multi (its 'gather' is a "
+                                  "device copy, the N-GPU step's is RCCL), wall clock per frame like ms_per_step")
         out["efficiency"] = round(t1["wall_ms"] / (n * tn_wall), 4)
         out["efficiency_kernel"] = round(t1["kernel_ms"] / (n * tn_kern), 4)
     print(json.dumps(out), flush=True)
@@ -456,7 +575,10 @@ def main(argv=None):
     except ValueError as e:
         log(f"error: {e}")
         sys.exit(2)
-    if mode == "inprocess":
+    if mode == "inprocess" or args.launch == "inprocess":
+        if world > 1:
+            log("error: --launch inprocess drives every GPU from one process; do not start it under a launcher")
+            sys.exit(2)
         return run_inprocess(args)
     # PTG_REHEARSAL=1: N ranks on one GPU with gloo (single-GPU box rehearsal
     # of the sharded path); the real multi-GPU run uses nccl (RCCL over xGMI)
@@ -470,6 +592,40 @@ def main(argv=None):
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+
+    # what the group is (N > 1): every rank's RCCL communicator (ncclCommCount,
+    # device, user rank) and its device's PCI bus id, all-gathered; a group
+    # of fewer ranks or distinct devices than --gpus ends the run (exit 3)
+    group = None
+    if world > 1:
+        dist.barrier()  # the communicator exists from here on
+        cnt, cdev, urank, why = (None, None, None, "gloo rehearsal: no RCCL communicator") if rehearsal \
+            else torch_rccl_info(local)
+        bus = bus_id_of(local)
+        rec = [cnt if cnt is not None else -1, cdev if cdev is not None else -1, urank if urank is not None else -1,
+               local] + list(bus.encode()[:32].ljust(32, b"\0"))
+        gdev = torch.device("cpu") if rehearsal else dev
+        mine = torch.tensor(rec, dtype=torch.int64, device=gdev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        recs = [t.cpu().tolist() for t in allr]
+        ranks = [r[0] if r[0] >= 0 else None for r in recs]
+        buses = [bytes(b for b in r[4:] if b).decode(errors="replace") for r in recs]
+        # distinct devices: one process per GPU, so the bus ids name them
+        bad = check_group(world, ranks, buses, buses, rehearsal)
+        group = {"rccl_ranks": None if rehearsal else ranks,
+                 "devices": [{"rank": k, "local_rank": r[3], "pci_bus_id": b,
+                              "rccl_device": r[1] if r[1] >= 0 else None,
+                              "rccl_user_rank": r[2] if r[2] >= 0 else None} for k, (r, b) in enumerate(zip(recs, buses))],
+                 "group_check": ("rehearsal: gloo on one GPU, no RCCL communicator" if rehearsal else
+                                 ("ok: " if not bad else "FAILED: ") +
+                                 f"{world} ranks on {len(set(buses))} distinct PCI bus ids, RCCL ranks {ranks}"
+                                 + (f" (ncclCommCount not determinable: {why})" if why and not rehearsal else ""))}
+        if bad:
+            if rank == 0:
+                log("error: the N-GPU group is not what the line would report: " + "; ".join(bad))
+            dist.destroy_process_group()
+            sys.exit(3)
 
     wl_name, scene, W, H, samps, nsub, spp = frame_config(args, world)
     scn = ptgpu.make_scene(scene, W, H)
@@ -588,6 +744,8 @@ def main(argv=None):
                                max(1, args.cpu_row_step), frame, ptgpu.DEFAULT_SEED, args.quality_rows)
         out["cpu_baseline"] = cpu
         out["launch"] = "torchrun" if world > 1 else "single"
+        if group is not None:
+            out.update(group)
         if per_rank is not None:
             out["per_rank"] = per_rank
         if t1_frame is not None:

@@ -84,7 +84,11 @@ struct ptg_multi {
     size_t image_cap = 0;
     std::vector<float> host;
     hipEvent_t t_unsharded = nullptr;  // root: the frame is un-sharded
-    bool timed = false;  // the events hold a completed ptg_multi_frame_device
+    // the events and the image hold a completed ptg_multi_frame_device of this
+    // size; cleared by every other frame call (render, passes, resolve), which
+    // write the image or start frames the events do not describe
+    bool timed = false;
+    int32_t frame_w = 0, frame_h = 0, frame_band_rows = 0;
     // a failure inside the RCCL group: the communicators were aborted and the
     // context refuses further frames (PTG_ERR_HIP) until destroyed
     bool broken = false;
@@ -98,8 +102,12 @@ int destroy(ptg_multi *m)
     if (!m)
         return PTG_OK;
     DeviceGuard g;
+    // every stream is drained before its buffers are freed -- a broken
+    // group's too: its communicators were aborted when the group failed, so
+    // nothing queued can block, and a failed frame's render kernels may still
+    // be running on the slabs
     for (Shard &s : m->shards) {
-        if (s.id < 0 || m->broken)  // a broken group's streams are not waited on
+        if (s.id < 0)
             continue;
         (void)hipSetDevice(s.id);
         if (s.stream)
@@ -383,6 +391,7 @@ int ptg_multi_render(ptg_multi *m, const ptg_params *params, double *image_rgb)
     int rc = check_frame(m, params);
     if (rc)
         return rc;
+    m->timed = false;  // the image / events no longer describe a frame_device frame
     if (!image_rgb)
         return fail(PTG_ERR_INVALID_ARGUMENT, "render_multi: image is NULL");
     DeviceGuard g;
@@ -409,6 +418,7 @@ int ptg_multi_reset_accumulation(ptg_multi *m, const ptg_params *params)
     int rc = check_frame(m, params);
     if (rc)
         return rc;
+    m->timed = false;  // the image / events no longer describe a frame_device frame
     DeviceGuard g;
     const int n = (int)m->shards.size();
     for (int k = 0; k < n; ++k) {
@@ -424,6 +434,7 @@ int ptg_multi_accumulate(ptg_multi *m, const ptg_params *params, int32_t sample_
     int rc = check_frame(m, params);
     if (rc)
         return rc;
+    m->timed = false;  // the image / events no longer describe a frame_device frame
     DeviceGuard g;
     const int n = (int)m->shards.size();
     for (int k = 0; k < n; ++k) {
@@ -440,6 +451,7 @@ int ptg_multi_resolve(ptg_multi *m, const ptg_params *params, int32_t samples_do
     int rc = check_frame(m, params);
     if (rc)
         return rc;
+    m->timed = false;  // the image / events no longer describe a frame_device frame
     if (!image_rgb)
         return fail(PTG_ERR_INVALID_ARGUMENT, "multi_resolve: image is NULL");
     DeviceGuard g;
@@ -492,6 +504,9 @@ int ptg_multi_frame_device(ptg_multi *m, const ptg_params *params, unsigned long
     if ((rc = sync_all(m)))
         return rc;
     m->timed = true;
+    m->frame_w = params->width;
+    m->frame_h = params->height;
+    m->frame_band_rows = params->band_rows;
     if (count && counters) {
         for (int i = 0; i < 4; ++i)
             counters[i] = 0;
@@ -528,13 +543,57 @@ int ptg_multi_image(ptg_multi *m, const ptg_params *params, float *image_rgb)
     if (rc)
         return rc;
     if (!image_rgb || !m->timed)
-        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_image: NULL image or no completed ptg_multi_frame_device");
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_image: NULL image or no completed ptg_multi_frame_device "
+                                              "(since the last render / pass / resolve)");
+    if (params->width != m->frame_w || params->height != m->frame_h || params->band_rows != m->frame_band_rows)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_image: params differ from the last frame's width, height or "
+                                              "band_rows");
     const size_t image_elems = (size_t)params->width * params->height * 3;
-    if (image_elems > m->image_cap)
-        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_image: params larger than the last frame");
     DeviceGuard g;
     MULTI_HIP(hipSetDevice(m->shards[0].id));
     MULTI_HIP(hipMemcpy(image_rgb, m->image, image_elems * sizeof(float), hipMemcpyDeviceToHost));
+    return PTG_OK;
+}
+
+int ptg_multi_comm_info(const ptg_multi *m, int32_t *ranks, int32_t *comm_devices, int32_t *user_ranks, int n)
+{
+    if (!m || !ranks || !comm_devices || !user_ranks)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_comm_info: NULL argument");
+    if (n != (int)m->shards.size())
+        return fail(PTG_ERR_INVALID_ARGUMENT, "multi_comm_info: one entry per shard");
+    for (int k = 0; k < n; ++k) {
+        const Shard &s = m->shards[k];
+        ranks[k] = 0;
+        comm_devices[k] = s.id;
+        user_ranks[k] = -1;
+        if (!s.comm)
+            continue;
+        int c = 0, dev = -1, ur = -1;
+        ncclResult_t r = ncclCommCount(s.comm, &c);
+        if (r == ncclSuccess)
+            r = ncclCommCuDevice(s.comm, &dev);
+        if (r == ncclSuccess)
+            r = ncclCommUserRank(s.comm, &ur);
+        if (r != ncclSuccess)
+            return nccl_fail("ncclCommCount/CuDevice/UserRank", r);
+        ranks[k] = c;
+        comm_devices[k] = dev;
+        user_ranks[k] = ur;
+    }
+    return PTG_OK;
+}
+
+int ptg_device_pci_bus_id(int device, char *buf, int len)
+{
+    if (!buf || len < 1)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "pci_bus_id: NULL or empty buffer");
+    buf[0] = '\0';
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(PTG_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= count)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "pci_bus_id: device ordinal out of range");
+    MULTI_HIP(hipDeviceGetPCIBusId(buf, len, device));
     return PTG_OK;
 }
 

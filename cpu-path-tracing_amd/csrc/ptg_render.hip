@@ -3193,6 +3193,26 @@ int ptg_render_device(ptg_context *ctx, const ptg_params *params, float *d_slab,
     return resolve ? launch_resolve(A, s) : PTG_OK;
 }
 
+int ptg_launch_info(ptg_context *ctx, const ptg_params *params, int64_t *info, int n_info)
+{
+    if (!ctx || !info || n_info < 1)
+        return fail(PTG_ERR_INVALID_ARGUMENT, "launch_info: NULL argument");
+    int rc = check_params(params);
+    if (rc)
+        return rc;
+    KArgs A;
+    int grid = 0;
+    if ((rc = fill_launch(ctx, params, A, grid)))
+        return rc;
+    const bool bvh = ctx->n > kLinearMax;
+    const int64_t v[PTG_LAUNCH_INFO_COUNT] = {
+        bvh ? 0 : A.box_mode, bvh ? 0 : A.box_walls_out, bvh ? 1 : 0, A.n_units, grid, A.n_levels,
+        A.needs_resolve ? 1 : 0, (int64_t)(A.pairs[0] | (A.pairs[1] << 1) | (A.pairs[2] << 2))};
+    for (int i = 0; i < n_info; ++i)
+        info[i] = i < PTG_LAUNCH_INFO_COUNT ? v[i] : 0;
+    return PTG_OK;
+}
+
 int ptg_accumulate_device(ptg_context *ctx, const ptg_params *params, int32_t sample_begin, int32_t sample_end,
                           unsigned long long *d_segments, void *stream)
 {

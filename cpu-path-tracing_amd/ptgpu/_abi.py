@@ -21,7 +21,8 @@ EXPORTS = (
     "ptg_reset_accumulation_device", "ptg_accumulate_device", "ptg_resolve_device", "ptg_scene_layout",
     "ptg_render_multi", "ptg_multi_create", "ptg_multi_destroy", "ptg_multi_render",
     "ptg_multi_reset_accumulation", "ptg_multi_accumulate", "ptg_multi_resolve", "ptg_multi_frame_device",
-    "ptg_multi_frame_timing", "ptg_multi_image", "ptg_math_probe_device",
+    "ptg_multi_frame_timing", "ptg_multi_image", "ptg_math_probe_device", "ptg_multi_comm_info",
+    "ptg_device_pci_bus_id", "ptg_launch_info",
 )
 
 
@@ -77,6 +78,9 @@ def lib():
             "ptg_multi_frame_device": (I, [P, C.POINTER(Params), P]),
             "ptg_multi_frame_timing": (I, [P, P, I, P]),
             "ptg_multi_image": (I, [P, C.POINTER(Params), P]),
+            "ptg_multi_comm_info": (I, [P, P, P, P, I]),
+            "ptg_device_pci_bus_id": (I, [I, C.c_char_p, I]),
+            "ptg_launch_info": (I, [P, C.POINTER(Params), P, I]),
             "ptg_multi_inject_gather_fault_": (I, [P, I]),
             # internal (tests): n shards on one device, gathered by device copies
             "ptg_multi_create_local_": (I, [P, C.c_size_t, P, I, I, C.POINTER(C.c_void_p)]),

@@ -195,6 +195,18 @@ class MultiContext:
         check(lib().ptg_multi_image(self._h, C.byref(params), out.ctypes.data_as(C.c_void_p)), "ptg_multi_image")
         return out.reshape(params.height, params.width, 3)
 
+    def comm_info(self):
+        """ptg_multi_comm_info: per shard (ncclCommCount, ncclCommCuDevice,
+        ncclCommUserRank) of its RCCL communicator -- (0, the shard's device,
+        -1) for local shards (no communicator)."""
+        n = self.n_devices
+        ranks = np.zeros(n, dtype=np.int32)
+        devs = np.zeros(n, dtype=np.int32)
+        user = np.zeros(n, dtype=np.int32)
+        check(lib().ptg_multi_comm_info(self._h, ranks.ctypes.data_as(C.c_void_p), devs.ctypes.data_as(C.c_void_p),
+                                        user.ctypes.data_as(C.c_void_p), n), "ptg_multi_comm_info")
+        return [(int(r), int(d), int(u)) for r, d, u in zip(ranks, devs, user)]
+
     def inject_gather_fault_(self, shard: int) -> None:
         """Tests: the next RCCL gather fails at `shard` (-1: off)."""
         check(lib().ptg_multi_inject_gather_fault_(self._h, int(shard)), "ptg_multi_inject_gather_fault_")
@@ -211,6 +223,13 @@ class MultiContext:
         check(lib().ptg_multi_resolve(self._h, C.byref(params), int(samples_done),
                                       self._image(image, params, np.float32)), "ptg_multi_resolve")
         return image
+
+
+def pci_bus_id(device: int) -> str:
+    """ptg_device_pci_bus_id: the PCI bus id of HIP device `device`."""
+    buf = C.create_string_buffer(64)
+    check(lib().ptg_device_pci_bus_id(int(device), buf, len(buf)), "ptg_device_pci_bus_id")
+    return buf.value.decode()
 
 
 def scene_layout(scn, cam):
@@ -284,6 +303,17 @@ class Context:
         check(lib().ptg_render_device(self._h, C.byref(params), C.c_void_p(out.data_ptr()),
                                       C.c_void_p(segments.data_ptr()) if segments is not None else None,
                                       C.c_void_p(s)), "ptg_render_device")
+
+    LAUNCH_INFO = ("box_mode", "box_walls_out", "bvh", "units", "workgroups", "levels", "resolve_pass",
+                   "wall_pairs")  # include/ptgpu.h ptg_launch_info
+
+    def launch_info(self, params: Params) -> dict:
+        """ptg_launch_info: how ptg_render_device would launch this frame
+        (scan mode, work units, levels) -- host-side, nothing is launched."""
+        v = np.zeros(len(self.LAUNCH_INFO), dtype=np.int64)
+        check(lib().ptg_launch_info(self._h, C.byref(params), v.ctypes.data_as(C.c_void_p), len(v)),
+              "ptg_launch_info")
+        return dict(zip(self.LAUNCH_INFO, (int(x) for x in v)))
 
     # ---- progressive accumulation (ptg_accumulate_device / ptg_resolve_device)
     def reset_accumulation(self, params: Params, stream=None) -> None:

@@ -184,13 +184,39 @@ int ptg_multi_resolve(ptg_multi *m, const ptg_params *params, int32_t samples_do
  * PTG_ERR_HIP; destroy the context. */
 int ptg_multi_frame_device(ptg_multi *m, const ptg_params *params, unsigned long long *counters);
 int ptg_multi_frame_timing(const ptg_multi *m, float *render_ms, int n_devices, float *frame_ms);
+/* The last ptg_multi_frame_device frame only: params must have the frame's
+ * width, height and band_rows (PTG_ERR_INVALID_ARGUMENT otherwise, and after
+ * any other frame call on the context). */
 int ptg_multi_image(ptg_multi *m, const ptg_params *params, float *image_rgb);
+/* What the context's RCCL group actually is (the proof behind a multi-GPU
+ * measurement): per shard k, ranks[k] = ncclCommCount of its communicator
+ * (0: no communicator -- local shards gathered by device copies, or an
+ * aborted group), comm_devices[k] = the HIP device its communicator runs on
+ * (ncclCommCuDevice; the shard's device for local shards), user_ranks[k] =
+ * ncclCommUserRank (-1 without a communicator).  n_devices must equal the
+ * context's shard count. */
+int ptg_multi_comm_info(const ptg_multi *m, int32_t *ranks, int32_t *comm_devices, int32_t *user_ranks,
+                        int n_devices);
+/* PCI bus id of a HIP device ("dddd:bb:dd.f", hipDeviceGetPCIBusId) into
+ * buf (len >= 16 recommended).  Distinct devices of a node have distinct ids. */
+int ptg_device_pci_bus_id(int device, char *buf, int len);
 
 /* ---- device-resident path (bench, multi-GPU) --------------------------
  * A context holds the prepared scene in HBM on one device. */
 int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, int device,
                        ptg_context **out);
 int ptg_context_destroy(ptg_context *ctx);
+
+/* How ptg_render_device would launch this frame (host-side, nothing is
+ * launched): info[0] box mode on (the linear scan's nearest-wall-first rule;
+ * the fast mode turns it off when a ray could start inside a wall),
+ * [1] box_walls_out (no ray can start inside a box wall: the fast mode's
+ * outside-only wall roots apply), [2] BVH scan (> 64 spheres), [3] work units,
+ * [4] workgroups, [5] unit levels, [6] an HBM accumulator + resolve pass,
+ * [7] wall-pair mask (x 1, y 2, z 4).  n_info <= PTG_LAUNCH_INFO_COUNT values
+ * are written (extra entries 0). */
+#define PTG_LAUNCH_INFO_COUNT 8
+int ptg_launch_info(ptg_context *ctx, const ptg_params *params, int64_t *info, int n_info);
 
 /* Rows in one shard's slab: ceil(bands / shard_count) * band_rows. */
 int ptg_shard_rows(int32_t height, int32_t band_rows, int32_t shard_count, int32_t *rows);

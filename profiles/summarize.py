@@ -63,14 +63,26 @@ def main(src, tag, kernel_sub="render_kernel"):
     out["sq"] = sq
     vgpr = [r for r in rows if kernel_sub in r["Kernel_Name"] and "render_kernel<true" not in r["Kernel_Name"]]
     if vgpr:
-        # rocprofv3's VGPR_Count field, as reported: on gfx950 it shows 32 for
-        # the linear render kernel, whose code object allocates 57 VGPRs
-        # (.vgpr_count in the ISA metadata; `make -C cpu-path-tracing_amd
-        # resource-usage`) -- the field is not the allocation, so it is
-        # recorded under its own name
+        # rocprofv3's VGPR_Count field reads 32 on gfx950 for both the linear
+        # (57 VGPRs) and the BVH render kernel (64): both allocate 64 (granule
+        # 8), encoded as 64/8 - 1 = 7 in the kernel descriptor, and (7 + 1) x 4
+        # = 32 is that field decoded with the older granule of 4.  The
+        # allocation is recorded from the code object's metadata instead
+        # (tools/kernel_resources.py), the profiler field under its own name.
         out["vgpr_rocprof_field"] = int(vgpr[0]["VGPR_Count"])
         out["sgpr"] = int(vgpr[0]["SGPR_Count"])
         out["lds_bytes"] = int(vgpr[0]["LDS_Block_Size"])
+    try:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+        import kernel_resources
+        out["vgpr_code_object"] = kernel_resources.render_kernel_vgprs()
+    except Exception as e:  # noqa: BLE001 -- optional (needs /opt/rocm's llvm tools)
+        out["vgpr_code_object"] = f"unavailable: {e}"
+    fp32 = [sq.get(k) for k in ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
+                                "SQ_INSTS_VALU_TRANS_F32")]
+    if all(v is not None for v in fp32) and sq.get("SQ_INSTS_VALU"):
+        # FP32 add/mul/fma/trans among all VALU instructions of the timed kernel
+        out["valu_fp32_share"] = sum(fp32) / sq["SQ_INSTS_VALU"]
     bench = os.path.join(src, "bench_trace.json")
     if os.path.exists(bench):
         out["bench"] = json.loads(open(bench).read().strip().splitlines()[-1])
@@ -97,6 +109,19 @@ def main(src, tag, kernel_sub="render_kernel"):
                 "VALUUtilization_pct": 100.0 * bz["SQ_THREAD_CYCLES_VALU"] / (bz["SQ_ACTIVE_INST_VALU"] * 64),
                 "MeanOccupancyPerCU_waves": bz["SQ_WAVE_CYCLES"] / cyc / cu,
             }
+    if "bench" in out and "roofline" in out["bench"]:
+        # the embedded bench line ran before this summary existed, so its
+        # PMC-derived fields came from the previous profile of the workload;
+        # restate them from THIS profile (the run-time values kept beside)
+        rf = out["bench"]["roofline"]
+        rf["pmc_fields_at_run_time"] = {k: rf.get(k) for k in ("traffic", "valu_issue_pct_profiled",
+                                                               "valu_fp32_share", "profile")}
+        rf["traffic"] = round(fetch_b + write_b)
+        if "derived" in out:
+            rf["valu_issue_pct_profiled"] = round(out["derived"]["valu_issue_pct"], 1)
+        if "valu_fp32_share" in out:
+            rf["valu_fp32_share"] = round(out["valu_fp32_share"], 4)
+        rf["profile"] = tag
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{tag}_summary.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
@@ -107,6 +132,8 @@ def main(src, tag, kernel_sub="render_kernel"):
         rec["valu_issue_pct"] = round(out["derived"]["valu_issue_pct"], 1)
         rec["valu_lane_utilisation_pct"] = round(out["derived"]["VALUUtilization_pct"], 1)
         rec["clock_GHz"] = round(out["derived"]["clock_GHz"], 3)
+    if "valu_fp32_share" in out:
+        rec["valu_fp32_share"] = round(out["valu_fp32_share"], 4)
     if "valu_insts_per_segment_wave_level" in out:
         rec["valu_insts_per_64_lane_segments"] = round(out["valu_insts_per_segment_wave_level"], 1)
     # one record per workload (bench.py load_pmc looks its workload up)

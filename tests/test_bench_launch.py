@@ -62,8 +62,47 @@ def test_main_inprocess_without_enough_gpus_exits_2(monkeypatch):
 
 
 def test_frame_config_defaults():
+    # one frame for every N: a scaling run's lines compare
+    # the metric's own box 1920x1080x1024spp frame
     a = bench.parse_args([])
-    assert bench.frame_config(a, 1) == ("bench", "box", 1920, 1080, 256, 2, 1024)
+    for n in (1, 2, 4, 8):
+        assert bench.frame_config(a, n) == ("bench", "box", 1920, 1080, 256, 2, 1024)
+    a = bench.parse_args(["--workload", "c4"])
     assert bench.frame_config(a, 8) == ("c4", "box", 3840, 2160, 1024, 2, 4096)
     a = bench.parse_args(["--workload", "c5"])
     assert bench.frame_config(a, 8)[:4] == ("c5", "synthetic:10000", 1920, 1080)
+
+
+def test_metric_names_the_rendered_frame():
+    assert bench.metric_of("box", 1920, 1080, 1024) == bench.METRIC
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert bench.METRIC == __import__("json").load(f)["metric"]
+    m = bench.metric_of("box", 3840, 2160, 4096)
+    assert m != bench.METRIC and "3840×2160×4096spp" in m and "box" in m
+    assert "1920×1080×1024spp" in bench.metric_of("box_mirror", 1920, 1080, 1024)
+    assert bench.metric_of("box_mirror", 1920, 1080, 1024) != bench.METRIC
+
+
+def test_group_check():
+    ok = bench.check_group(4, [4, 4, 4, 4], [0, 1, 2, 3], ["a", "b", "c", "d"], False)
+    assert ok == []
+    assert bench.check_group(4, [1, 1, 1, 1], [0, 1, 2, 3], ["a", "b", "c", "d"], False)  # 4 one-rank comms
+    assert bench.check_group(4, [4, 4, 4, 4], [0, 0, 1, 1], ["a", "a", "b", "b"], False)  # shared devices
+    assert bench.check_group(2, [2, 2], [0, 1], ["a", "a"], False)  # one bus id twice
+    # not determinable (None) is not evidence either way; rehearsals exempt
+    assert bench.check_group(2, [None, None], [0, 1], ["a", "b"], False) == []
+    assert bench.check_group(4, [], [0, 0, 0, 0], ["a"] * 4, True) == []
+    assert bench.check_group(1, [1], [0], ["a"], False) == []
+
+
+def test_launch_inprocess_flag():
+    assert bench.parse_args(["--launch", "inprocess"]).launch == "inprocess"
+    assert bench.parse_args([]).launch == "auto"
+
+
+def test_roofline_fields():
+    pmc = {"valu_fp32_share": 0.49, "hbm_bytes_per_launch": 1, "tag": "x"}
+    s_bar, r = bench.roofline(100, 1200, 8 * 1200, 0, 100, 1e-6, 8, pmc)
+    assert abs(s_bar - 12.0) < 1e-12
+    assert r["valu_fp32_share"] == 0.49
+    assert abs(r["frac_nonpacked"] / r["frac"] - bench.PEAK_FP32_TFLOPS / bench.PEAK_FP32_NONPACKED_TFLOPS) < 1e-3

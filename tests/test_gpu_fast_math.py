@@ -254,3 +254,29 @@ def test_fast_no_out_of_range_radiance(name):
         res[mode] = [int(v) for v in cnt.cpu().tolist()]
     assert res[0][3] == 0 and res[EXACT][3] == 0, res
     assert abs(res[0][0] - res[EXACT][0]) <= 1e-3 * res[EXACT][0], res
+
+
+def test_box_mode_fallback_is_taken():
+    """the fast mode's box-mode wall test keeps only the outside
+    root, so it must be OFF whenever a ray can start inside a wall -- asserted
+    directly (ptg_launch_info), not only through the image RMSE of a scene
+    whose trapped rays are noisy either way.  box_glass_back (a dielectric
+    back wall, which transmitted rays enter): the fast mode scans generically,
+    the exact mode keeps box mode with its full root rule; box and box_mirror
+    run box mode with outside-only walls in both modes; > 64 spheres: BVH."""
+    _require_gpu()
+    W, H, samps = 64, 48, 4
+    expect = {  # scene: (fast box_mode, exact box_mode, box_walls_out)
+        "box": (1, 1, 1), "box_mirror": (1, 1, 1), "box_glass_back": (0, 1, 0), "simple": (0, 0, 0)}
+    for name, (fast_bm, exact_bm, out) in expect.items():
+        scn = _scene(name, W, H)
+        cam = ptgpu.camera.with_config(scn.camera_parameters)
+        with ptgpu.Context(scn, cam, device=0) as ctx:
+            f = ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED))
+            e = ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED, flags=EXACT))
+        assert (f["box_mode"], e["box_mode"], f["box_walls_out"]) == (fast_bm, exact_bm, out), (name, f, e)
+        assert f["bvh"] == 0 and f["units"] > 0 and f["workgroups"] > 0
+    scn = ptgpu.make_scene("synthetic:10000", W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    with ptgpu.Context(scn, cam, device=0) as ctx:
+        assert ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED))["bvh"] == 1

@@ -178,3 +178,73 @@ def test_multi_gather_fault_aborts_the_group():
     img = np.zeros((H * W, 3))
     ptgpu.render(scn, cam, img, W, H, samps)
     assert img.mean() > 0
+
+
+@pytest.mark.parametrize("n", [2])
+def test_multi_gather_fault_at_last_shard_aborts_queued_gathers(n):
+    """the case the abort exists for -- ncclGather calls of earlier
+    ranks already queued in the group when a later one fails.  Needs n
+    distinct GPUs (skipped on the 1-GPU box; the driver's 8-GPU node runs
+    it): the error, the later refusal and a close() that returns."""
+    _require_gpu()
+    if torch.cuda.device_count() < n:
+        pytest.skip(f"needs {n} GPUs, {torch.cuda.device_count()} visible")
+    W, H, samps = 32, 16, 2
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    p = ptgpu.make_params(W, H, samps, 2, SEED, 1)
+    m = ptgpu.MultiContext(scn, cam, list(range(n)))
+    assert [r for r, _, _ in m.comm_info()] == [n] * n
+    m.frame_device(p)
+    m.inject_gather_fault_(n - 1)
+    with pytest.raises(ptgpu.PtgError, match="ncclGather"):
+        m.frame_device(p)
+    with pytest.raises(ptgpu.PtgError, match="aborted"):
+        m.frame_device(p)
+    m.close()
+    img = np.zeros((H * W, 3))
+    ptgpu.render(scn, cam, img, W, H, samps)
+    assert img.mean() > 0
+
+
+def test_multi_comm_info_and_bus_ids():
+    """what a multi-GPU line reports about its group --
+    ncclCommCount / ncclCommCuDevice / ncclCommUserRank of each shard's
+    communicator (here a one-rank group on device 0) and the PCI bus id; local
+    shards have no communicator."""
+    _require_gpu()
+    W, H = 16, 8
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    with ptgpu.MultiContext(scn, cam, [0]) as m:
+        assert m.comm_info() == [(1, 0, 0)]
+    with ptgpu.MultiContext(scn, cam, [0], local_shards=3) as m:
+        assert m.comm_info() == [(0, 0, -1)] * 3
+    bus = ptgpu.pci_bus_id(0)
+    assert len(bus) >= 7 and bus.count(":") >= 1, bus
+    with pytest.raises(ptgpu.PtgError):
+        ptgpu.pci_bus_id(torch.cuda.device_count())
+
+
+def test_multi_image_only_for_the_last_device_frame():
+    """ptg_multi_image returns the last ptg_multi_frame_device frame
+    only -- params of another size are refused, and so is any call after a
+    render / pass / resolve wrote the image buffer."""
+    _require_gpu()
+    W, H, samps = 24, 12, 2
+    scn = ptgpu.box_scene(W, H)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    p = ptgpu.make_params(W, H, samps, 2, SEED, 1)
+    with ptgpu.MultiContext(scn, cam, [0], local_shards=2) as m:
+        m.frame_device(p)
+        m.image(p)
+        m.frame_timing()
+        with pytest.raises(ptgpu.PtgError, match="differ"):
+            m.image(ptgpu.make_params(W // 2, H // 2, samps, 2, SEED, 1))
+        with pytest.raises(ptgpu.PtgError, match="differ"):
+            m.image(ptgpu.make_params(W, H, samps, 2, SEED, 2))
+        m.render(np.zeros((H * W, 3)), p)
+        with pytest.raises(ptgpu.PtgError, match="no completed"):
+            m.image(p)
+        with pytest.raises(ptgpu.PtgError, match="no completed"):
+            m.frame_timing()
