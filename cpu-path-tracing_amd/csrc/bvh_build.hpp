@@ -383,6 +383,12 @@ inline uint16_t half_ceil(double x)
 // the largest surface, in place, so the children keep the binary tree's
 // near-first order for the octant (order_bvh).  Nodes are in depth-first
 // pre-order (a node's children follow it).
+#ifndef PTG_BVH_ONE_LAYOUT
+// 1: ONE wide layout for all ray octants (octant 0's child order, planes
+// stored min first); the kernel puts each slab's near plane first per lane
+// with one v_perm_b32 per axis.  0: one layout per octant (8 copies).
+#define PTG_BVH_ONE_LAYOUT 0
+#endif
 #ifndef PTG_WIDE_N
 #define PTG_WIDE_N 4  // children per wide node (the kernel's walk is written for 4; 8: design studies, tools/)
 #endif
@@ -438,8 +444,18 @@ struct WideGrid {
         uint32_t a[3], b[3];
         for (int c = 0; c < 3; ++c) {
             const bool f = (flip >> c) & 1;
+#if PTG_BVH_ONE_LAYOUT
+            // one layout for every octant (the kernel orders each slab's planes
+            // per lane): an inverted box would read as the whole grid, so the
+            // empty slot is a point at grid value +60000 on every axis, outside
+            // the root box (|h| <= 30000) -- a ray meets it only by passing
+            // exactly through it, and then visits an empty leaf (count 0)
+            (void)f;
+            a[c] = b[c] = 0x7B53u;
+#else
             a[c] = f ? 0xFB53u : 0x7B53u;  // near plane -/+60000 and far plane +/-60000: the
             b[c] = f ? 0x7B53u : 0xFB53u;  // octant's rays enter the slab after leaving it
+#endif
         }
         BvhNodeQ q;
         q.xy_min = a[0] | (a[1] << 16);

@@ -420,6 +420,9 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 #ifndef PTG_WALL_OUT
 #define PTG_WALL_OUT 1  // fast mode, box mode: the nearest wall's outside-only root (KArgs::box_walls_out)
 #endif
+#ifndef PTG_SMALL_UNROLL
+#define PTG_SMALL_UNROLL 0  // linear scan: three small spheres as straight-line code (A/B)
+#endif
 #ifndef PTG_BOX_WALL_LOOP
 #define PTG_BOX_WALL_LOOP 1  // box mode: extra walls one per lane per pass, with the exact cull (0: per-axis branches)
 #endif
@@ -720,6 +723,17 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     }
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
+#if PTG_SMALL_UNROLL
+    // three small spheres (the box scenes): straight-line code on one LDS
+    // base address (the records at constant offsets), no loop control
+    if (A.n - i == 3) {
+        const LinRec *r0 = recs + i;
+        test_rec(r0, std::integral_constant<int, kSmall>{});
+        test_rec(r0 + 1, std::integral_constant<int, kSmall>{});
+        test_rec(r0 + 2, std::integral_constant<int, kSmall>{});
+        i = A.n;
+    }
+#endif
     for (; i < A.n; ++i)
         test(i, std::integral_constant<int, kSmall>{});
     tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
@@ -891,9 +905,13 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 #if PTG_BVH_WIDE
     // the wide layouts store each box near-plane first for their octant:
     // all 8 layouts exist (bvh_oct_mask = 7)
+#if PTG_BVH_ONE_LAYOUT
+    tr.ni = A.n_nodes > 0 ? 0 : -1;  // the one layout, for every octant
+#else
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
     tr.ni = A.n_nodes > 0 ? (int)(oct << A.bvh_shift) : -1;
+#endif
     tr.s0 = -1;
     tr.s1 = -1;
 #if PTG_BVH_STACK >= 3
@@ -917,6 +935,39 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 struct SlabRay {
     float sx, sy, sz, bx, by, bz;
 };
+#if PTG_BVH_ONE_LAYOUT
+// The one layout stores each child box min-plane first: words {x0, y0},
+// {z0, x1}, {y1, z1} (low half first).  Per lane and axis one v_perm_b32
+// gathers the axis's two planes into one word, near plane in the low half:
+// for d_k >= 0 the min plane, else the max plane.  Selector bytes index
+// {S0, S1} as S1 = 0..3, S0 = 4..7.
+//   x: S0 = w0 (x0 at 4,5), S1 = w1 (x1 at 2,3)  -> {x0, x1} 0x03020504, {x1, x0} 0x05040302
+//   y: S0 = w0 (y0 at 6,7), S1 = w2 (y1 at 0,1)  -> {y0, y1} 0x01000706, {y1, y0} 0x07060100
+//   z: S0 = w1 (z0 at 4,5), S1 = w2 (z1 at 2,3)  -> {z0, z1} 0x03020504, {z1, z0} 0x05040302
+// The selector is a bitfield insert on the sign mask of the slab scale
+// (sign of d_k): 2 VALU per axis per node step, kept out of the walk's
+// registers.
+__device__ __forceinline__ unsigned near_sel(float s, unsigned pos, unsigned neg)
+{
+    const unsigned m = (unsigned)(__float_as_int(s) >> 31);  // all ones for d_k < 0
+    return (m & neg) | (~m & pos);  // v_bfi_b32
+}
+__device__ __forceinline__ bool box_hit_one(const u32x4 q, const SlabRay &r, const float tcap)
+{
+    const unsigned px = __builtin_amdgcn_perm(q.x, q.y, near_sel(r.sx, 0x03020504u, 0x05040302u));
+    const unsigned py = __builtin_amdgcn_perm(q.x, q.z, near_sel(r.sy, 0x01000706u, 0x07060100u));
+    const unsigned pz = __builtin_amdgcn_perm(q.y, q.z, near_sel(r.sz, 0x03020504u, 0x05040302u));
+    const float tnx = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(px & 0xFFFFu)), r.sx, r.bx);
+    const float tny = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(py & 0xFFFFu)), r.sy, r.by);
+    const float tnz = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(pz & 0xFFFFu)), r.sz, r.bz);
+    const float tfx = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(px >> 16)), r.sx, r.bx);
+    const float tfy = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(py >> 16)), r.sy, r.by);
+    const float tfz = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(pz >> 16)), r.sz, r.bz);
+    const float t_in = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, 0.0f));
+    const float t_out = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, tcap));
+    return !(t_in > t_out);
+}
+#endif
 __device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
 {
     const float ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
@@ -1020,8 +1071,13 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
 #if PTG_NODE_CASCADE
     // slots before the walk's position (ni & 3) are not tested again
     const int s = tr.ni & 3;
+#if PTG_BVH_ONE_LAYOUT
+    const bool h0 = box_hit_one(q0, r, tcap) & (s == 0), h1 = box_hit_one(q1, r, tcap) & (s <= 1),
+               h2 = box_hit_one(q2, r, tcap) & (s <= 2), h3 = box_hit_one(q3, r, tcap);
+#else
     const bool h0 = box_hit_sorted(q0, r, tcap) & (s == 0), h1 = box_hit_sorted(q1, r, tcap) & (s <= 1),
                h2 = box_hit_sorted(q2, r, tcap) & (s <= 2), h3 = box_hit_sorted(q3, r, tcap);
+#endif
     // the words of the first three hits in slot order (-1: none) and the
     // slots of the second and third, shifted in from the last slot: every
     // step is a v_cndmask on its box test's lane mask (the hit mask with
@@ -2928,7 +2984,9 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         while ((size_t(1) << shift) <= n_recs)
             ++shift;
 #if PTG_BVH_WIDE
-        const size_t n_layouts = 8;  // near-plane-first boxes: one layout per octant
+        // near-plane-first boxes: one layout per octant, or one for all
+        // (PTG_BVH_ONE_LAYOUT: the kernel orders the planes per lane)
+        const size_t n_layouts = PTG_BVH_ONE_LAYOUT ? 1 : 8;
 #else
         const size_t n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
 #endif

@@ -124,15 +124,28 @@ def test_primitive_accuracy_and_exact_mode_bits():
 # error falls as 1/sqrt(spp)); C5 is held to the bar at its own 1024 spp in
 # test_gpu_baseline_configs.py
 SCENES = [("simple", 200, 150, 16, True), ("box", 160, 120, 32, True), ("box_mirror", 160, 120, 32, True),
-          ("box_glass_back", 160, 120, 32, True), ("synthetic:300", 128, 72, 16, True),
+          ("box_glass_back", 160, 120, 32, True), ("box_cam_near_wall", 160, 120, 32, True),
+          ("synthetic:300", 128, 72, 16, True),
           ("synthetic:10000", 96, 54, 16, False)]
 
 
 def _scene(name, W, H):
     """box_glass_back: box_scene with a dielectric back wall -- rays enter
-    that wall, so the fast mode may not use box mode's outside-only wall
-    test (KArgs::box_walls_out) and scans generically; the exact mode keeps
-    box mode."""
+    that wall; box mode is off in both arithmetic modes (a dielectric wall
+    is neither paired nor a clear single wall), the scan is generic.
+    box_cam_near_wall: box_scene with the camera 0.1 below the ceiling's
+    tangent plane, inside its lens reach (2 lens radii = 0.2): box mode holds
+    (the walls are clear of the camera), but a lens-offset camera ray may
+    start inside the ceiling sphere, so the fast mode's outside-only wall
+    roots do not apply (box_walls_out = 0) and the fast mode falls back to
+    the generic scan, while the exact mode keeps box mode with the full root
+    rule."""
+    if name == "box_cam_near_wall":
+        scn = ptgpu.make_scene("box", W, H)
+        cfg = scn.camera_parameters
+        cfg.position = (cfg.position[0], 0.3, cfg.position[2])
+        cfg.direction = (cfg.direction[0], 0.3, cfg.direction[2])
+        return scn
     if name == "box_glass_back":
         scn = ptgpu.make_scene("box", W, H)
         sp = list(scn.spheres)
@@ -260,14 +273,16 @@ def test_box_mode_fallback_is_taken():
     """the fast mode's box-mode wall test keeps only the outside
     root, so it must be OFF whenever a ray can start inside a wall -- asserted
     directly (ptg_launch_info), not only through the image RMSE of a scene
-    whose trapped rays are noisy either way.  box_glass_back (a dielectric
-    back wall, which transmitted rays enter): the fast mode scans generically,
-    the exact mode keeps box mode with its full root rule; box and box_mirror
-    run box mode with outside-only walls in both modes; > 64 spheres: BVH."""
+    whose trapped rays are noisy either way.  box_cam_near_wall (lens rays may
+    start inside the ceiling): the fast mode scans generically, the exact
+    mode keeps box mode with its full root rule; box_glass_back: no box mode
+    in either; box and box_mirror run box mode with outside-only walls in
+    both modes; > 64 spheres: BVH."""
     _require_gpu()
     W, H, samps = 64, 48, 4
     expect = {  # scene: (fast box_mode, exact box_mode, box_walls_out)
-        "box": (1, 1, 1), "box_mirror": (1, 1, 1), "box_glass_back": (0, 1, 0), "simple": (0, 0, 0)}
+        "box": (1, 1, 1), "box_mirror": (1, 1, 1), "box_cam_near_wall": (0, 1, 0), "box_glass_back": (0, 0, 0),
+        "simple": (0, 0, 0)}
     for name, (fast_bm, exact_bm, out) in expect.items():
         scn = _scene(name, W, H)
         cam = ptgpu.camera.with_config(scn.camera_parameters)

@@ -11,7 +11,7 @@ for r in $(seq 1 $rounds); do
       lib=cpu-path-tracing_amd/build/libptgpu_$v.so; [ $v = main ] && lib=cpu-path-tracing_amd/libptgpu.so
       out=gpurun_out/ab_${tag}_$v.json
       PTGPU_LIB=$lib timeout -k 10 150 python bench.py --cpu-baseline off $w > $out 2>/dev/null || { echo "$v [$w] failed"; exit 1; }
-      python -c "import json;d=json.load(open('$out'));r=d['roofline'];print('$v', d['config']['workload'], 'round $r', d['ms_per_step'], r['kernel_ms'], r['frac'])"
+      python -c "import json;d=json.load(open('$out'));r=d['roofline'];print('$v', d['config']['workload'], 'round $r', d['ms_per_step'], r['kernel_ms'], r['frac'], 'box/seg', r.get('box_tests_per_segment'), 'sph/seg', r.get('sphere_tests_per_segment'))"
     done
   done
 done

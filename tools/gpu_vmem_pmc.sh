@@ -38,4 +38,7 @@ if c.get("TCP_TA_TCP_STATE_READ_sum"):
     print("avg TCP wave latency (cycles):", c["TCP_TCP_LATENCY_sum"] / c["TCP_TA_TCP_STATE_READ_sum"])
 if c.get("TA_TOTAL_WAVEFRONTS_sum"):
     print("vector-memory wave instructions per CU-cycle:", c["TA_TOTAL_WAVEFRONTS_sum"] / 256 / g)
+    if c.get("TCP_TOTAL_READ_sum"):
+        print("TCP reads per wave-level load (TCP_TOTAL_READ / TA_TOTAL_WAVEFRONTS):",
+              c["TCP_TOTAL_READ_sum"] / c["TA_TOTAL_WAVEFRONTS_sum"])
 PY
