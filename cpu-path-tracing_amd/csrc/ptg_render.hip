@@ -171,6 +171,11 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_DG_SKIP
 #define PTG_DG_SKIP 1  // shade: skip the diffuse/dielectric block when no lane of the wave needs it
 #endif
+#ifndef PTG_DG_SPLIT
+// shade: a wave with no dielectric lane runs the diffuse sampler alone
+// (measured slower: box +0.4 %, A/B r05c)
+#define PTG_DG_SPLIT 0
+#endif
 #ifndef PTG_SMALL_DISC_SKIP
 #define PTG_SMALL_DISC_SKIP 1  // linear scan: skip a small sphere's root when no lane's disc >= 0 (box -0.9 %, box_mirror -2.1 %, simple -7 %; also skipping spheres behind every lane: +0.1-0.5 %)
 #endif
@@ -420,8 +425,26 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 #ifndef PTG_WALL_OUT
 #define PTG_WALL_OUT 1  // fast mode, box mode: the nearest wall's outside-only root (KArgs::box_walls_out)
 #endif
+#ifndef PTG_BVH_LAYOUT_PAD
+// wide BVH: records of padding between the octant layouts (a multiple of 4;
+// 0: layouts exactly 2^k records apart, so the 8 copies of a node alias in
+// the caches' set index)
+#define PTG_BVH_LAYOUT_PAD 0
+#endif
+#ifndef PTG_BVH_INTERLEAVE
+// wide BVH: the 8 octant layouts interleaved node by node -- node j of
+// layout k at 8 j + k, the copies of a node in one 512-B block.  Laid out
+// 2^k records apart they aliased in the L1's set index: C5 225.9-226.2 ->
+// 218.3-218.5 ms (A/B r05c; a 4-record pad between the layouts gets 219.1-219.3)
+#define PTG_BVH_INTERLEAVE 1
+#endif
 #ifndef PTG_SMALL_UNROLL
-#define PTG_SMALL_UNROLL 0  // linear scan: three small spheres as straight-line code (A/B)
+// linear scan: three small spheres (the box scenes) as straight-line code on
+// one LDS base address (box -0.6 %, box_mirror -0.7 %, A/B r05b/r05c)
+#define PTG_SMALL_UNROLL 1
+#endif
+#ifndef PTG_LEAF_NT
+#define PTG_LEAF_NT 0  // BVH leaf sphere records loaded non-temporal (A/B)
 #endif
 #ifndef PTG_BOX_WALL_LOOP
 #define PTG_BOX_WALL_LOOP 1  // box mode: extra walls one per lane per pass, with the exact cull (0: per-axis branches)
@@ -910,7 +933,12 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 #else
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
-    tr.ni = A.n_nodes > 0 ? (int)(oct << A.bvh_shift) : -1;
+#if PTG_BVH_INTERLEAVE
+    tr.ni = A.n_nodes > 0 ? (int)(oct << 2) : -1;  // layout k's root: interleaved node k
+#else
+    // layout k at record k * (2^shift + PTG_BVH_LAYOUT_PAD)
+    tr.ni = A.n_nodes > 0 ? (int)((oct << A.bvh_shift) + oct * PTG_BVH_LAYOUT_PAD) : -1;
+#endif
 #endif
     tr.s0 = -1;
     tr.s1 = -1;
@@ -1229,7 +1257,16 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
     float tbm = tb * kCullScale;
     for (int j = 0; j < cnt; ++j) {
         const unsigned off = (unsigned)(f + j) << 4;
-        const float t = root_lex<false, kExact>(*(const float4 *)(sph + off), float4{}, o, d, a, tb, tbm);
+#if PTG_LEAF_NT
+        // non-temporal: the leaf records stream past the L1, whose lines
+        // then hold the walk's upper node levels (A/B)
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        const f32x4 v = __builtin_nontemporal_load((const f32x4 *)(sph + off));
+        const float4 rec = make_float4(v.x, v.y, v.z, v.w);
+#else
+        const float4 rec = *(const float4 *)(sph + off);
+#endif
+        const float t = root_lex<false, kExact>(rec, float4{}, o, d, a, tb, tbm);
         if (t <= tb) {  // the scene index is read only for a candidate that wins or ties
             update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
             tbm = tb * kCullScale;
@@ -1477,6 +1514,31 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #if PTG_BLOCK_STATS == 3  // debug: wave cycles of the diffuse/dielectric block in [14]
         const unsigned long long dg_t0 = clock64();
 #endif
+#if PTG_DG_SPLIT
+        // a wave without dielectric lanes runs the diffuse sampler alone:
+        // the same operations for every diffuse lane as the shared code
+        // below (bit for bit), without the dielectric half of its selects
+        // and the refraction vector (wave-uniform, exact)
+        if (__ballot(isG) == 0ull) {
+            if (isD) {
+                const uint32_t m_phi = draw_bits(st);
+                const float ra = draw(st);
+                float cp, sp;
+                Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
+                const f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
+                const float r1 = Math<kExact>::rsqrt(dot3(uu, uu));
+                const f3 v1 = mk3(uu.x * r1, uu.y * r1, uu.z * r1);
+                const float s2 = Math<kExact>::sqrt0(ra);
+                const float s3 = Math<kExact>::sqrt(1.0f - ra);
+                const f3 vv = cross3(nn, v1);
+                const float cs = cp * s2, ss = sp * s2;
+                nd = mk3(__builtin_fmaf(nn.x, s3, __builtin_fmaf(vv.x, ss, v1.x * cs)),
+                         __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
+                         __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
+            }
+        } else
+#endif
+        {
         float cp = 0.0f, sp = 0.0f, ra = 0.0f;
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
             const uint32_t m_phi = draw_bits(st);
@@ -1518,6 +1580,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         } else {  // refraction, main.cpp:93-96
             nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
                      __builtin_fmaf(nn.z, -s3, perp.z));
+        }
         }
 #if PTG_BLOCK_STATS == 3
         {
@@ -2990,12 +3053,41 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
 #else
         const size_t n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
 #endif
-        const size_t stride = size_t(1) << shift;
+        // (+ PTG_BVH_LAYOUT_PAD records: the octant layouts' copies of one
+        // node are not a power of two apart)
+        const size_t stride = PTG_BVH_WIDE && PTG_BVH_INTERLEAVE
+                                  ? n_recs  // (interleaved: 8 x n_recs records in all, no layout stride)
+                                  : (size_t(1) << shift) + (PTG_BVH_WIDE ? PTG_BVH_LAYOUT_PAD : 0);
         const size_t off_cont = off_q + n_layouts * stride * sizeof(BvhNodeQ);
         const size_t total = off_cont + (PTG_BVH_WIDE ? n_layouts * stride / kWide * sizeof(int32_t) : 0) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
+#if PTG_BVH_WIDE && PTG_BVH_INTERLEAVE
+        // the 8 layouts interleaved node by node: node j of layout k at
+        // interleaved node 8 j + k, so the copies of one node share a 512-B
+        // block instead of aliasing 2^shift records apart
+        static_assert(!PTG_BVH_ONE_LAYOUT, "interleaving needs the octant layouts");
+        {
+            auto ilv = [](int32_t local, int k) { return ((local >> 2) * 8 + k) * 4 + (local & 3); };
+            for (int k = 0; k < 8; ++k) {
+                std::vector<BvhNodeQ> qk = wide_bvh(b, k, 0);
+                const std::vector<int32_t> ck = wide_conts(qk, 0);
+                for (size_t r = 0; r < qk.size(); ++r) {
+                    BvhNodeQ z = qk[r];
+                    if (z.word >= 0)
+                        z.word = ilv(z.word, k);
+                    std::memcpy(blob.data() + off_q + (size_t)ilv((int32_t)r, k) * sizeof(BvhNodeQ), &z, sizeof(z));
+                }
+                for (size_t j = 0; j < ck.size(); ++j) {
+                    const int32_t c = ck[j] >= 0 ? ilv(ck[j], k) : ck[j];
+                    std::memcpy(blob.data() + off_cont + (j * 8 + (size_t)k) * sizeof(int32_t), &c, sizeof(c));
+                }
+            }
+        }
+        for (size_t k = 0; k < 0; ++k) {
+#else
         for (size_t k = 0; k < n_layouts; ++k) {
+#endif
             std::vector<BvhNodeQ> qk;
 #if PTG_BVH_WIDE
             qk = wide_bvh(b, (int)k, (int32_t)(k * stride));  // same root box: same grid, absolute words
