@@ -384,8 +384,15 @@ __device__ __forceinline__ void camera_ray(const CamC &C, const Lane &L, uint32_
     // camera.cpp:19-30: rejection sample of the unit disk (2 draws per try)
     float px, py;
     do {
+#if PTG_RR_INT
+        // 2 u - 1 with u = m 2^-24: 2^-23 m - 1, the same exact product
+        // (the draw's scale folded into the fma)
+        px = __builtin_fmaf(0x1p-23f, (float)draw_bits(st), -1.0f);
+        py = __builtin_fmaf(0x1p-23f, (float)draw_bits(st), -1.0f);
+#else
         px = __builtin_fmaf(2.0f, draw(st), -1.0f);
         py = __builtin_fmaf(2.0f, draw(st), -1.0f);
+#endif
     } while (__builtin_fmaf(py, py, px * px) >= 1.0f);
     // camera.cpp:34-37 (offset = rd*s + rd*t, the reference's lens quirk)
     float sst = fs + ft;
@@ -442,6 +449,9 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 // linear scan: three small spheres (the box scenes) as straight-line code on
 // one LDS base address (box -0.6 %, box_mirror -0.7 %, A/B r05b/r05c)
 #define PTG_SMALL_UNROLL 1
+#endif
+#ifndef PTG_RR_INT
+#define PTG_RR_INT 0  // Russian roulette as an integer compare of the draw's 24 bits (A/B)
 #endif
 #ifndef PTG_SMALL_AC
 #define PTG_SMALL_AC 0  // fast mode, small spheres: the near root as (hb^2 - disc) / (a qq) (A/B)
@@ -1505,9 +1515,15 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // masked -- its next ray and state are discarded (the early return's
     // merge had cost state copies and exec-mask blocks)
     uint32_t st_rr = st;
+#if PTG_RR_INT
+    const uint32_t m_rr = draw_bits(st_rr);  // u = m_rr 2^-24; s0.w holds ceil(p 2^24) (prepare_scene)
+    st = rr ? st_rr : st;
+    const bool killed = rr & !(m_rr < __float_as_uint(s0.w));
+#else
     const float u_rr = draw(st_rr);
     st = rr ? st_rr : st;
     const bool killed = rr & !(u_rr < s0.w);  // (box -0.6 %, box_mirror -1.0 %)
+#endif
     T = mk3(T.x * (rr ? c3.x : c2.x), T.y * (rr ? c3.y : c2.y), T.z * (rr ? c3.z : c2.z));
     // BRDF samplers (main.cpp:44-97).  Diffuse and dielectric lanes share the
     // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
@@ -2469,7 +2485,18 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
         int32_t mat = sp.material;
         float matf;
         std::memcpy(&matf, &mat, 4);
+#if PTG_RR_INT
+        // Russian roulette as an integer compare (main.cpp:130-131, u < p):
+        // u = m 2^-24 exactly (m the draw's 24-bit integer), so u < p <=> m <
+        // p 2^24 <=> m < ceil(p 2^24) -- the same decisions as the oracle's
+        // float compare, without the draw's convert and scale
+        uint32_t p24 = !(p > 0.0f) ? 0u : (p >= 1.0f ? (1u << 24) : (uint32_t)std::ceil((double)p * 16777216.0));
+        float p24f;
+        std::memcpy(&p24f, &p24, 4);
+        r.s0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], p24f);
+#else
         r.s0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], p);
+#endif
         r.s1 = make_float4((float)sp.emission[0], (float)sp.emission[1], (float)sp.emission[2], matf);
         r.s2 = make_float4(cx, cy, cz, (float)(1.0 / R));
         r.s3 = make_float4(rx, ry, rz, 0.0f);

@@ -85,6 +85,23 @@ def test_image_vs_reference_arithmetic(cfg, name, W, H, samps, ystep, guard, mod
         assert np.array_equal(gpu, b), (cfg, int((gpu != b).any(axis=2).sum()), "pixels differ")
 
 
+def test_c3_exact_every_8th_row_bit_exact():
+    """C3 (box_mirror 1920x1080 at 1024 spp, the deep-bounce config) in the
+    exact arithmetic mode: every 8th row of the frame (135 of 1,080, all
+    their samples) equals the fp32 restatement (Mode B) bit for bit -- the
+    whole frame is in tools/full_frame_parity.py (too long for the suite:
+    ~4 min of CPU on the box's 16 threads)."""
+    _require_gpu()
+    W, H, samps, ystep = 1920, 1080, 256, 8
+    scn = ptgpu.make_scene("box_mirror", W, H)
+    cam, sp, ca = _arrays(scn)
+    gpu = _render(scn, cam, W, H, samps, flags=EXACT)
+    ys = np.arange(ystep // 2, H, ystep)  # image-space y
+    b, _ = po.render_xs_f32(sp, ca, W, H, samps, 2, SEED, rows=(ystep // 2, H, ystep), nthreads=NT)
+    g, r = gpu[H - 1 - ys], b[H - 1 - ys]
+    assert np.array_equal(g, r), int((g != r).any(axis=2).sum())
+
+
 @pytest.mark.parametrize("name", ["box", "box_mirror", "simple", "synthetic:300"])
 def test_no_out_of_range_radiance(name):
     """PTG_FLAG_COUNT_NONFINITE: no path of the shipped scenes has a NaN,
