@@ -451,7 +451,10 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 #define PTG_SMALL_UNROLL 1
 #endif
 #ifndef PTG_RR_INT
-#define PTG_RR_INT 0  // Russian roulette as an integer compare of the draw's 24 bits (A/B)
+// Russian roulette as an integer compare of the draw's 24 bits, the disk
+// draws' 2^-24 folded into their fma (exact: the same decisions and values;
+// box -0.5 %, box_mirror -0.6 %, A/B r05j)
+#define PTG_RR_INT 1
 #endif
 #ifndef PTG_SMALL_AC
 #define PTG_SMALL_AC 0  // fast mode, small spheres: the near root as (hb^2 - disc) / (a qq) (A/B)
