@@ -456,6 +456,13 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 // box -0.5 %, box_mirror -0.6 %, A/B r05j)
 #define PTG_RR_INT 1
 #endif
+#ifndef PTG_DG_NOINIT
+// shade: the diffuse sampler's values not zero-initialised for the other
+// lanes (3 v_mov fewer per segment in waves with diffuse lanes: box -0.6 %,
+// box_mirror -0.4 %, A/B r05k)
+#define PTG_DG_NOINIT 1
+#endif
+
 #ifndef PTG_SMALL_AC
 #define PTG_SMALL_AC 0  // fast mode, small spheres: the near root as (hb^2 - disc) / (a qq) (A/B)
 #endif
@@ -1572,7 +1579,13 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         } else
 #endif
         {
+#if PTG_DG_NOINIT
+        // read only where isD (the ?: operands and the isD branch below):
+        // no initial values to set for the other lanes
+        float cp, sp, ra;
+#else
         float cp = 0.0f, sp = 0.0f, ra = 0.0f;
+#endif
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
             const uint32_t m_phi = draw_bits(st);
             ra = draw(st);
