@@ -463,6 +463,9 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 #define PTG_DG_NOINIT 1
 #endif
 
+#ifndef PTG_NODE_POP_SEL
+#define PTG_NODE_POP_SEL 0  // BVH node step: the stack pop as selects, not a divergent branch (A/B)
+#endif
 #ifndef PTG_SMALL_AC
 #define PTG_SMALL_AC 0  // fast mode, small spheres: the near root as (hb^2 - disc) / (a qq) (A/B)
 #endif
@@ -1098,6 +1101,9 @@ __device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, 
 // when a leaf was parked: ni = kPopLater then, and the leaf phase pops.
 // Selections are branch-free (v_cndmask).
 constexpr int kPopLater = -2;
+#if PTG_LEAF_DONE_SEL
+__device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bool need, const int keep);
+#endif
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
                                               ScanCount &cnt, const u32x4 *lds_root = nullptr, int root_mask = 0,
@@ -1209,6 +1215,15 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     tr.s0 = push ? (full ? -1 : e) : s0;
     tr.s1 = push ? (full ? -1 : s0) : tr.s1;
 #endif
+#if PTG_NODE_POP_SEL && PTG_LEAF_DONE_SEL
+    // the pop as selects for every stepping lane (bvh_pop_sel, as the leaf
+    // completion): no divergent branch whose join copies the stack registers
+    const bool need = next == -1;
+    next = bvh_pop_sel(cont, tr, need, next);
+    const bool lf = need & (next < kPopLater);  // a leaf from the stack
+    tr.pend = lf ? (next & 0x7FFFFFFF) : tr.pend;
+    next = lf ? kPopLater : next;
+#else
     if (next == -1) {
         next = bvh_pop(cont, tr);
         if (next < kPopLater) {  // a leaf from the stack
@@ -1216,6 +1231,7 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
             next = kPopLater;
         }
     }
+#endif
     tr.ni = next;
 }
 
