@@ -239,6 +239,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_WAVE_STATS
 #define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
 #endif
+#ifndef PTG_SMALL_SGPR
+#define PTG_SMALL_SGPR 0  // the three small spheres' geometry from kernel arguments (SGPRs), not LDS (A/B r05p: box +0.4 %, box_mirror -0.2 %; not kept)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -287,6 +290,12 @@ struct KArgs {
     // tangent planes (+-inf: none); pair_lo/hi bound the room on every
     // axis (+-kFarPlane where open)
     int box_mode;
+    // PTG_SMALL_SGPR: the three small spheres' geometry {C, -R^2} when the
+    // scan ends with exactly three (the box scenes), read as kernel
+    // arguments (scalar registers), not from LDS
+#if PTG_SMALL_SGPR
+    float small_geo[3][4];
+#endif
     int rec_plus[3], rec_minus[3];  // byte offsets of the records
     float plane_plus[3], plane_minus[3];
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
@@ -463,6 +472,17 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 #define PTG_DG_NOINIT 1
 #endif
 
+#ifndef PTG_KN_MASKS
+// box mode: the nearest plane's axis kept as lane masks and its wall-table
+// byte offset selected directly (the axis index had been re-compared and
+// re-multiplied); with PTG_NEED_NOINF box -2.1 %, box_mirror -2.1 % (A/B r05p)
+#define PTG_KN_MASKS 1
+#endif
+
+#ifndef PTG_NEED_NOINF
+#define PTG_NEED_NOINF 1  // box mode (with PTG_KN_MASKS): need[] without the u < inf guard (exact, see need[])
+#endif
+
 #ifndef PTG_NODE_POP_SEL
 #define PTG_NODE_POP_SEL 0  // BVH node step: the stack pop as selects, not a divergent branch (A/B)
 #endif
@@ -487,12 +507,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
     const LinRec *best = recs + A.n;
-    auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
-                        const bool valid = true, const int ks = 0) {
+    auto test_geo = [&](const LinRec *r, const float4 g0, const float4 g1, auto kind_tag, const float un = 0.0f,
+                        const float vn = 0.0f, const bool valid = true, const int ks = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
         // r is wave-uniform, except for a pair's walls / box mode
-        float4 g0 = r->g.g0;
-        float4 g1 = r->g.g1;
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
         float ed = dot3(e, d);
         float ee = dot3(e, e);
@@ -604,6 +622,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         bq = win ? den : bq;
         best = win ? r : best;
     };
+    auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
+                        const bool valid = true, const int ks = 0) {
+        test_geo(r, r->g.g0, r->g.g1, kind_tag, un, vn, valid, ks);
+    };
     auto test = [&](const int i, auto kind_tag) { test_rec(recs + i, kind_tag); };
     // scan order: axis-anchored walls (x, y, z), general huge spheres, small
     // spheres (host: prepare_scan_order)
@@ -644,6 +666,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // k's + wall (2k) and - wall (2k + 1), -1 where missing
         const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
         float u[3], v[3];
+#if PTG_KN_MASKS
+        bool posk[3];
+#endif
         for (int k = 0; k < 3; ++k) {
             // the uniform plane / record values stay in SGPRs: select values,
             // not kernel-argument addresses (that became per-lane loads)
@@ -658,7 +683,27 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             const float up = pp - comp(o, k), um = comp(o, k) - pm;
             u[k] = pos ? up : um;
             v[k] = __builtin_fabsf(dk);
+#if PTG_KN_MASKS
+            posk[k] = pos;
+#endif
         }
+#if PTG_KN_MASKS
+        // the same selection as below, kept as lane masks (is_k) and the wall
+        // table's byte offset of the selected wall (8 k, + 4 for the - wall),
+        // not as an axis index re-compared and re-multiplied
+        float un = u[0], vn = v[0];
+        int offn = posk[0] ? 0 : 4;
+        const bool n1 = u[1] * vn < un * v[1];
+        un = n1 ? u[1] : un;
+        vn = n1 ? v[1] : vn;
+        offn = n1 ? (posk[1] ? 8 : 12) : offn;
+        const bool n2 = u[2] * vn < un * v[2];
+        un = n2 ? u[2] : un;
+        vn = n2 ? v[2] : vn;
+        offn = n2 ? (posk[2] ? 16 : 20) : offn;
+        const bool isk[3] = {!(n1 | n2), (bool)(n1 & !n2), n2};
+        const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls) + offn);
+#else
         float un = u[0], vn = v[0];
         int kn = 0;
         for (int k = 1; k < 3; ++k) {
@@ -674,6 +719,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // v_cndmask 0/1 and a shift)
         const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls + 2 * kn) +
                                                       (comp(d, kn) >= 0.0f ? 0 : 4));
+#endif
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
@@ -686,7 +732,16 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // holds for any v (also guarded explicitly by u < inf -- a test of
             // values: selecting the kernel-argument record offsets per lane
             // compiled to three dependent global loads)
+#if PTG_KN_MASKS && PTG_NEED_NOINF
+            // (no u < inf guard: a missing wall's need is false unless bn v
+            // is NaN, and the pass below masks a missing wall's test by its
+            // table offset -1 -- the same results)
+            need[k] = !isk[k] & !(bn * v[k] < u[k] * bqm);
+#elif PTG_KN_MASKS
+            need[k] = !isk[k] & (u[k] < HUGE_VALF) & !(bn * v[k] < u[k] * bqm);
+#else
             need[k] = (k != kn) & (u[k] < HUGE_VALF) & !(bn * v[k] < u[k] * bqm);
+#endif
         }
         // a wall the ray moves away from can be hit only from beyond its
         // tangent plane (outside the room's bound on that side -- after a
@@ -788,9 +843,16 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     // base address (the records at constant offsets), no loop control
     if (A.n - i == 3) {
         const LinRec *r0 = recs + i;
+#if PTG_SMALL_SGPR
+        // the records' geometry words as kernel arguments (the same values)
+        for (int k = 0; k < 3; ++k)
+            test_geo(r0 + k, make_float4(A.small_geo[k][0], A.small_geo[k][1], A.small_geo[k][2], 0.0f),
+                     make_float4(0.0f, 0.0f, 0.0f, A.small_geo[k][3]), std::integral_constant<int, kSmall>{});
+#else
         test_rec(r0, std::integral_constant<int, kSmall>{});
         test_rec(r0 + 1, std::integral_constant<int, kSmall>{});
         test_rec(r0 + 2, std::integral_constant<int, kSmall>{});
+#endif
         i = A.n;
     }
 #endif
@@ -3097,6 +3159,16 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     }
     A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
     A.end_big = order.end_big;
+#if PTG_SMALL_SGPR
+    if (linear && (int)n_spheres - order.end_big == 3)
+        for (int k = 0; k < 3; ++k) {
+            const GeoRec &g = lin[order.end_big + k].g;
+            A.small_geo[k][0] = g.g0.x;
+            A.small_geo[k][1] = g.g0.y;
+            A.small_geo[k][2] = g.g0.z;
+            A.small_geo[k][3] = g.g1.w;
+        }
+#endif
     A.box_walls_out = order.box_walls_out;
     if ((int)n_spheres > kLinearMax) {
         std::vector<char> huge(n_spheres);
