@@ -242,6 +242,16 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_SMALL_SGPR
 #define PTG_SMALL_SGPR 0  // the three small spheres' geometry from kernel arguments (SGPRs), not LDS (A/B r05p: box +0.4 %, box_mirror -0.2 %; not kept)
 #endif
+#ifndef PTG_WALL_GEO
+// box mode: the walls' geometry copied into a table indexed by (axis, side)
+// after the offset table, the record's byte offset in g1.x and NaN geometry
+// for a missing wall (no win) -- one LDS round trip per scan instead of two
+// (with PTG_DEPTH_EARLY: box -1.0 %, box_mirror -1.0 %, A/B r05q)
+#define PTG_WALL_GEO 1
+#endif
+#ifndef PTG_DEPTH_EARLY
+#define PTG_DEPTH_EARLY 1  // shade: depth counted before the sky branch (no per-branch copy; A/B r05q)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -702,7 +712,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         vn = n2 ? v[2] : vn;
         offn = n2 ? (posk[2] ? 16 : 20) : offn;
         const bool isk[3] = {!(n1 | n2), (bool)(n1 & !n2), n2};
+#if !PTG_WALL_GEO
         const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls) + offn);
+#endif
 #else
         float un = u[0], vn = v[0];
         int kn = 0;
@@ -723,8 +735,19 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
+#if PTG_WALL_GEO && PTG_KN_MASKS
+        {
+            // 32-B geometry entries, entry 2 k + side at 8 offn bytes
+            const GeoRec *wg = reinterpret_cast<const GeoRec *>(recs + A.n + 2);
+            const GeoRec &g = *reinterpret_cast<const GeoRec *>(reinterpret_cast<const char *>(wg) + 8 * offn);
+            const float4 g0 = g.g0, g1 = g.g1;
+            test_geo(rec_at(__float_as_int(g1.x)), g0, g1,
+                     std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{}, un, vn);
+        }
+#else
         test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{},
                  un, vn, in >= 0);
+#endif
         const float bqm = bq * kPlaneMargin;
         bool need[3];
         for (int k = 0; k < 3; ++k) {
@@ -1574,6 +1597,12 @@ template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st)
 {
+#if PTG_DEPTH_EARLY
+    // the segment count first, for every lane: a sky lane's path ends here
+    // (its depth is reset by the refill), so the value is only read below --
+    // no per-branch copy of the loop-carried register
+    depth += 1;
+#endif
     if (!hit) {  // main.cpp:115-120: sky
         f3 ud = norm3m<kExact>(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -1597,7 +1626,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // main.cpp:128-139: Russian roulette after depth 4.  Both colour records
     // are loaded and selected (3 selects instead of address arithmetic)
     const float4 c2 = S.s2, c3 = S.s3;
-    const bool rr = depth > kRRThreshold;
+    const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
     // Russian roulette without an early return: the roulette's draw advances the state of the
     // rr lanes only (a select), and a killed lane runs on with its materials
     // masked -- its next ray and state are discarded (the early return's
@@ -1723,7 +1752,9 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     }
     o = p;
     d = nd;
+#if !PTG_DEPTH_EARLY
     depth += 1;
+#endif
     return killed | (depth >= kDepthLimit);
 }
 
@@ -1789,7 +1820,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             trig = lds_trig;
         }
 #endif
-        for (int i = threadIdx.x; i <= A.n + 1; i += kBlock)  // n records + the sentinel + the wall table
+        for (int i = threadIdx.x; i <= A.n + 1 + 2 * PTG_WALL_GEO; i += kBlock)  // n records + the sentinel + the wall table(s)
             lds_lin[i] = A.lin[i];
         recs = lds_lin;
     }
@@ -3096,7 +3127,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     std::vector<LinRec> lin;
     if (linear) {  // the scan's record order, interleaved, + the no-hit sentinel
         prepare_scan_order(spheres, (int)n_spheres, cam, geo, shade, axis, lgeo, lshade, order);
-        lin.resize(n_spheres + 2);  // + the box-mode wall table (scene_scan)
+        lin.resize(n_spheres + 2 + 2 * PTG_WALL_GEO);  // + the box-mode wall table(s) (scene_scan)
         std::memset(lin.data(), 0, lin.size() * sizeof(LinRec));
         for (size_t i = 0; i < n_spheres; ++i)
             lin[i] = LinRec{lgeo[i], lshade[i]};
@@ -3106,6 +3137,24 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             walls[2 * k + 1] = order.rec_minus[k];
         }
         std::memcpy(&lin[n_spheres + 1], walls, sizeof(walls));
+#if PTG_WALL_GEO
+        // entry 2 k + side: the wall's geometry, g1.x = its record's byte
+        // offset; a missing wall: NaN geometry (its test never wins), offset 0
+        GeoRec wg[6];
+        for (int e = 0; e < 6; ++e) {
+            const float qnan = __builtin_nanf("");
+            const int off = walls[e];
+            if (order.box_mode && off >= 0 && off / (int)sizeof(LinRec) < (int)n_spheres) {
+                wg[e] = lgeo[off / (int)sizeof(LinRec)];
+                std::memcpy(&wg[e].g1.x, &off, 4);
+            } else {
+                wg[e].g0 = make_float4(qnan, qnan, qnan, qnan);
+                wg[e].g1 = make_float4(0.0f, qnan, qnan, qnan);
+            }
+        }
+        static_assert(sizeof(wg) <= 2 * sizeof(LinRec), "wall geometry table size");
+        std::memcpy(&lin[n_spheres + 2], wg, sizeof(wg));
+#endif
     }
     ptg_context *ctx = new ptg_context();
     ctx->device = dev;
@@ -3389,7 +3438,7 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     if (grid <= 0)
         return PTG_OK;
     const bool bvh = A.n > kLinearMax;
-    const size_t lds = bvh ? 0 : (size_t)(A.n + 2) * sizeof(LinRec);
+    const size_t lds = bvh ? 0 : (size_t)(A.n + 2 + 2 * PTG_WALL_GEO) * sizeof(LinRec);
     // the exact mode's sin/cos table has its own LDS (render_kernel)
     const int sel = (count ? 4 : 0) | (bvh ? 2 : 0) | (A.exact_math ? 1 : 0);
     switch (sel) {
