@@ -252,6 +252,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_DEPTH_EARLY
 #define PTG_DEPTH_EARLY 1  // shade: depth counted before the sky branch (no per-branch copy; A/B r05q)
 #endif
+#ifndef PTG_WALLS_LAST
+#define PTG_WALLS_LAST 0  // fast box mode: the small spheres tested before the extra walls (A/B)
+#endif
+#ifndef PTG_SMALL_PREFETCH
+#define PTG_SMALL_PREFETCH 1  // the three small spheres' records read one test ahead, the first at the scan's start (box -0.2 %, box_mirror -0.3 %, A/B r05t)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -663,6 +669,42 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #ifndef PTG_ASSUME_BOX_MODE
 #define PTG_ASSUME_BOX_MODE 0  // analysis builds only (tools/isa_breakdown.py): box mode on, the other scan compiled out
 #endif
+#if PTG_SMALL_PREFETCH
+    // the first small sphere's geometry (the records after the huge ones;
+    // always in bounds: the sentinel follows the last record)
+    const float4 pf_g0 = recs[A.end_big].g.g0, pf_g1 = recs[A.end_big].g.g1;
+#endif
+    // the small spheres [i, n) (i = n after)
+    auto small_spheres = [&](int &i) {
+#if PTG_SMALL_UNROLL
+        // three small spheres (the box scenes): straight-line code on one LDS
+        // base address (the records at constant offsets), no loop control
+        if (A.n - i == 3) {
+            const LinRec *r0 = recs + i;
+#if PTG_SMALL_SGPR
+            // the records' geometry words as kernel arguments (the same values)
+            for (int k = 0; k < 3; ++k)
+                test_geo(r0 + k, make_float4(A.small_geo[k][0], A.small_geo[k][1], A.small_geo[k][2], 0.0f),
+                         make_float4(0.0f, 0.0f, 0.0f, A.small_geo[k][3]), std::integral_constant<int, kSmall>{});
+#elif PTG_SMALL_PREFETCH
+            // each record's geometry read one test ahead (its LDS latency
+            // behind the previous test; the first at the scan's start)
+            const float4 a1 = r0[1].g.g0, b1 = r0[1].g.g1;
+            test_geo(r0, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
+            const float4 a2 = r0[2].g.g0, b2 = r0[2].g.g1;
+            test_geo(r0 + 1, a1, b1, std::integral_constant<int, kSmall>{});
+            test_geo(r0 + 2, a2, b2, std::integral_constant<int, kSmall>{});
+#else
+            test_rec(r0, std::integral_constant<int, kSmall>{});
+            test_rec(r0 + 1, std::integral_constant<int, kSmall>{});
+            test_rec(r0 + 2, std::integral_constant<int, kSmall>{});
+#endif
+            i = A.n;
+        }
+#endif
+        for (; i < A.n; ++i)
+            test(i, std::integral_constant<int, kSmall>{});
+    };
     if (PTG_ASSUME_BOX_MODE || A.box_mode) {
         // Box mode (DESIGN.md "box mode"): per axis the wall the ray moves
         // toward and the distance u/v to its tangent plane; the wall of the
@@ -747,6 +789,17 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #else
         test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{},
                  un, vn, in >= 0);
+#endif
+#if PTG_WALLS_LAST
+        // fast mode: the small spheres before the extra walls (box mode has
+        // no other huge sphere: they follow the walls in the scan), so the
+        // wall test's LDS read overlaps their first instructions and need[]
+        // culls against the nearer winner; only exact ties between an extra
+        // wall and a small sphere can resolve differently
+        if constexpr (!kExact) {
+            int j = A.end_ax[2];
+            small_spheres(j);
+        }
 #endif
         const float bqm = bq * kPlaneMargin;
         bool need[3];
@@ -853,7 +906,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             }
 #endif
         }
-        i = A.end_ax[2];
+        i = (PTG_WALLS_LAST && !kExact) ? A.n : A.end_ax[2];
     } else {
         axis_group(std::integral_constant<int, kAxX>{});
         axis_group(std::integral_constant<int, kAxY>{});
@@ -861,26 +914,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     }
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
-#if PTG_SMALL_UNROLL
-    // three small spheres (the box scenes): straight-line code on one LDS
-    // base address (the records at constant offsets), no loop control
-    if (A.n - i == 3) {
-        const LinRec *r0 = recs + i;
-#if PTG_SMALL_SGPR
-        // the records' geometry words as kernel arguments (the same values)
-        for (int k = 0; k < 3; ++k)
-            test_geo(r0 + k, make_float4(A.small_geo[k][0], A.small_geo[k][1], A.small_geo[k][2], 0.0f),
-                     make_float4(0.0f, 0.0f, 0.0f, A.small_geo[k][3]), std::integral_constant<int, kSmall>{});
-#else
-        test_rec(r0, std::integral_constant<int, kSmall>{});
-        test_rec(r0 + 1, std::integral_constant<int, kSmall>{});
-        test_rec(r0 + 2, std::integral_constant<int, kSmall>{});
-#endif
-        i = A.n;
-    }
-#endif
-    for (; i < A.n; ++i)
-        test(i, std::integral_constant<int, kSmall>{});
+    small_spheres(i);
     tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
     return best;
 }
