@@ -258,6 +258,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_SMALL_PREFETCH
 #define PTG_SMALL_PREFETCH 1  // the three small spheres' records read one test ahead, the first at the scan's start (box -0.2 %, box_mirror -0.3 %, A/B r05t)
 #endif
+#ifndef PTG_INROOM_EARLY
+#define PTG_INROOM_EARLY 0  // box mode: the room-bound compares before the wall test (A/B)
+#endif
+#ifndef PTG_SHADE_EARLY
+#define PTG_SHADE_EARLY 0  // shade: the hit record's reads first, the roulette's draw in their shadow (A/B; needs PTG_RR_INT)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -777,12 +783,23 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
+#if PTG_INROOM_EARLY
+        bool in_room;
+#endif
 #if PTG_WALL_GEO && PTG_KN_MASKS
         {
             // 32-B geometry entries, entry 2 k + side at 8 offn bytes
             const GeoRec *wg = reinterpret_cast<const GeoRec *>(recs + A.n + 2);
             const GeoRec &g = *reinterpret_cast<const GeoRec *>(reinterpret_cast<const char *>(wg) + 8 * offn);
             const float4 g0 = g.g0, g1 = g.g1;
+#if PTG_INROOM_EARLY
+            // (independent of the wall test: its compares issued while the
+            // wall record's LDS read is in flight -- held there by a
+            // scheduling barrier)
+            in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
+                      (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             test_geo(rec_at(__float_as_int(g1.x)), g0, g1,
                      std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{}, un, vn);
         }
@@ -823,8 +840,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // tangent plane (outside the room's bound on that side -- after a
         // bounce off a curved wall far from its tangent point, frequent in
         // box_mirror's mirror tube); a missing wall's bound is +-kFarPlane
+#if !PTG_INROOM_EARLY
         const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
                              (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
+#endif
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             PTG_STAT(3);
 #if PTG_BLOCK_STATS == 3  // debug: wave cycles of the extra-wall block in [15]
@@ -1648,6 +1667,15 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     }
     const ShadeRec &S = *hit;
     float4 s0 = S.s0, s1 = S.s1;
+#if PTG_SHADE_EARLY
+    // the record's reads issued first, the roulette's draw (independent of
+    // them) computed while they are in flight -- held there by a scheduling
+    // barrier
+    const float4 c2 = S.s2, c3 = S.s3;
+    uint32_t st_rr = st;
+    const uint32_t m_rr = draw_bits(st_rr);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // hit_record.cpp:3-12
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
     // hit_record.cpp:6 (p - C).norm() as (p - C) * (1/R): p lies on the sphere
@@ -1659,15 +1687,21 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
     // main.cpp:128-139: Russian roulette after depth 4.  Both colour records
     // are loaded and selected (3 selects instead of address arithmetic)
+#if !PTG_SHADE_EARLY
     const float4 c2 = S.s2, c3 = S.s3;
+#endif
     const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
     // Russian roulette without an early return: the roulette's draw advances the state of the
     // rr lanes only (a select), and a killed lane runs on with its materials
     // masked -- its next ray and state are discarded (the early return's
     // merge had cost state copies and exec-mask blocks)
+#if !PTG_SHADE_EARLY
     uint32_t st_rr = st;
+#endif
 #if PTG_RR_INT
+#if !PTG_SHADE_EARLY
     const uint32_t m_rr = draw_bits(st_rr);  // u = m_rr 2^-24; s0.w holds ceil(p 2^24) (prepare_scene)
+#endif
     st = rr ? st_rr : st;
     const bool killed = rr & !(m_rr < __float_as_uint(s0.w));
 #else
