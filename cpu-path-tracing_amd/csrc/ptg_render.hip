@@ -264,6 +264,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_SHADE_EARLY
 #define PTG_SHADE_EARLY 0  // shade: the hit record's reads first, the roulette's draw in their shadow (A/B; needs PTG_RR_INT)
 #endif
+#ifndef PTG_LIN_UNROLL2
+#define PTG_LIN_UNROLL2 0  // linear kernel: the main loop's body twice (A/B)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -2204,6 +2207,19 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     path_done();
             }
             refill();
+#if PTG_LIN_UNROLL2
+            // the loop body twice: the two copies can hold the ray's
+            // loop-carried registers in alternating places (no join copies)
+            if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+                break;
+            if (item >= 0) {
+                if constexpr (kCount)
+                    segs += 1;
+                if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
+                    path_done();
+            }
+            refill();
+#endif
 #endif
         }
 #if PTG_BLOCK_STATS == 3
