@@ -267,6 +267,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_LIN_UNROLL2
 #define PTG_LIN_UNROLL2 0  // linear kernel: the main loop's body twice (A/B)
 #endif
+#ifndef PTG_D_INPLACE
+#define PTG_D_INPLACE 0  // shade: the next direction written into d in place (A/B)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -1721,7 +1724,14 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     const bool isD = !killed & (mat == PTG_DIFFUSE);
     const bool isG = !killed & (mat == PTG_DIELECTRIC);
     bool spec = !killed & (mat == PTG_SPECULAR);
+#if PTG_D_INPLACE
+    // the next direction written into d in place: each lane's sampler writes
+    // it after the lane's last read of d (a refraction only where no
+    // reflection follows), so the loop-carried register needs no copy
+    f3 &nd = d;
+#else
     f3 nd = d;  // every lane sets it below (mirror lanes in the spec block)
+#endif
     // a wave with only mirror lanes skips the diffuse/dielectric work
     // (wave-uniform, exact: those lanes' values are all overwritten)
 #if PTG_DG_SKIP
@@ -1801,7 +1811,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
             nd = mk3(__builtin_fmaf(nn.x, s3, __builtin_fmaf(vv.x, ss, v1.x * cs)),
                      __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
                      __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
-        } else {  // refraction, main.cpp:93-96
+        } else
+#if PTG_D_INPLACE
+        if (!spec)
+#endif
+        {  // refraction, main.cpp:93-96
             nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
                      __builtin_fmaf(nn.z, -s3, perp.z));
         }
