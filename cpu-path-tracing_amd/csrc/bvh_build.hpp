@@ -466,6 +466,88 @@ struct WideGrid {
     }
 };
 
+// PTG_BVH_Q8 (ptg_render.hip): the same wide node in 48 B -- three 16-B
+// loads per node step instead of four (the walk is bound by its load
+// instructions: tools/node_width_bench.hip).  Dwords 0-3: the 4 child words;
+// 4-5: the node's grid origin per axis as binary16 in units of 256 grid
+// steps (x, y | z) and per axis F = E + 16 (5 bits at 16, 21, 26 of dword 5);
+// 6-11: the 24 plane bytes q, plane = origin + q 2^E grid units, rounded
+// outward from the binary16 planes of the 64-B record.  A child's planes are
+// three pairs (near x, near y), (near z, far x), (far y, far z): pair 3 c + m.
+// Dword i holds pairs 2 i (bytes 0, 2) and 2 i + 1 (bytes 1, 3), so one
+// v_and_b32 / v_perm_b32 turns a pair into the binary16 pair {q_A, q_B}
+// 2^-24 (subnormal halves, exact in v_fma_mix_f32): the kernel reads the
+// planes as t = h (sx 2^(E + 24)) + (origin sx + bx) with the slab scale
+// sx taken 256 times larger (KArgs::q_scale).  An empty slot: near q beyond
+// far q for the octant (255 / 0, swapped on a flipped axis).
+struct WideQ8 {
+    uint32_t w[12];
+};
+inline WideQ8 wide_q8(const BvhNodeQ *r, int flip)
+{
+    WideQ8 o{};
+    double lo[kWide][3], hi[kWide][3];
+    double L[3] = {INFINITY, INFINITY, INFINITY}, H[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool used[kWide];
+    for (int c = 0; c < kWide; ++c) {
+        used[c] = r[c].word != kWideEmpty;
+        const uint32_t a[3] = {r[c].xy_min & 0xFFFFu, r[c].xy_min >> 16, r[c].z_min_x_max & 0xFFFFu};
+        const uint32_t b[3] = {r[c].z_min_x_max >> 16, r[c].y_max_z_max & 0xFFFFu, r[c].y_max_z_max >> 16};
+        for (int k = 0; k < 3; ++k) {
+            const double n = half_value((uint16_t)a[k]), f = half_value((uint16_t)b[k]);
+            const bool fl = (flip >> k) & 1;
+            lo[c][k] = fl ? f : n;
+            hi[c][k] = fl ? n : f;
+            if (used[c]) {
+                L[k] = std::min(L[k], lo[c][k]);
+                H[k] = std::max(H[k], hi[c][k]);
+            }
+        }
+    }
+    uint16_t oh[3];
+    int fe[3];
+    uint8_t q[kWide][6];  // near x, y, z, far x, y, z
+    for (int k = 0; k < 3; ++k) {
+        if (!(L[k] <= H[k]))
+            L[k] = H[k] = 0.0;  // no used child
+        oh[k] = half_floor(L[k] / 256.0);
+        const double O = 256.0 * half_value(oh[k]);  // <= L
+        int E = -16;
+        while (E < 15 && O + 255.0 * std::ldexp(1.0, E) < H[k])
+            ++E;
+        fe[k] = E + 16;
+        const double D = std::ldexp(1.0, E);
+        const bool fl = (flip >> k) & 1;
+        for (int c = 0; c < kWide; ++c) {
+            int ql, qh;
+            if (used[c]) {
+                ql = std::max(0, std::min(255, (int)std::floor((lo[c][k] - O) / D)));
+                qh = std::max(0, std::min(255, (int)std::ceil((hi[c][k] - O) / D)));
+                while (ql > 0 && O + ql * D > lo[c][k])  // exact in double: O a scaled binary16, D a power of two
+                    --ql;
+                while (qh < 255 && O + qh * D < hi[c][k])
+                    ++qh;
+            } else {  // empty: the octant's rays enter the slab after leaving it
+                ql = 255;
+                qh = 0;
+            }
+            q[c][k] = (uint8_t)(fl ? qh : ql);
+            q[c][3 + k] = (uint8_t)(fl ? ql : qh);
+        }
+    }
+    for (int c = 0; c < kWide; ++c)
+        o.w[c] = (uint32_t)r[c].word;
+    o.w[4] = (uint32_t)oh[0] | ((uint32_t)oh[1] << 16);
+    o.w[5] = (uint32_t)oh[2] | ((uint32_t)fe[0] << 16) | ((uint32_t)fe[1] << 21) | ((uint32_t)fe[2] << 26);
+    // pair p = 3 c + m: (near x, near y), (near z, far x), (far y, far z)
+    static const int kA[3] = {0, 2, 4}, kB[3] = {1, 3, 5};
+    for (int p = 0; p < 12; ++p) {
+        const int c = p / 3, m = p % 3, i = p / 2, odd = p & 1;
+        o.w[6 + i] |= ((uint32_t)q[c][kA[m]] << (8 * odd)) | ((uint32_t)q[c][kB[m]] << (16 + 8 * odd));
+    }
+    return o;
+}
+
 namespace detail {
 
 inline void wide_children(const BvhBuild &b, int i, int octant, int kids[kWide], int &nk)

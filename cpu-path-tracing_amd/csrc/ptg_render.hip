@@ -475,6 +475,14 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 // the caches' set index)
 #define PTG_BVH_LAYOUT_PAD 0
 #endif
+#ifndef PTG_BVH_Q8
+// wide BVH: 48-B nodes (8-bit planes on a per-node grid, bvh_build.hpp
+// wide_q8): three 16-B loads per node step instead of four (A/B)
+#define PTG_BVH_Q8 0
+#endif
+#ifndef PTG_BVH_Q8_STRIDE
+#define PTG_BVH_Q8_STRIDE 48  // bytes per 48-B node in the array (64: 16-B padded, line-aligned; A/B)
+#endif
 #ifndef PTG_BVH_INTERLEAVE
 // wide BVH: the 8 octant layouts interleaved node by node -- node j of
 // layout k at 8 j + k, the copies of a node in one 512-B block.  Laid out
@@ -1249,12 +1257,40 @@ constexpr int kPopLater = -2;
 __device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bool need, const int keep);
 #endif
 template <bool kCount>
-__device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
+__device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r_in, BvhTrav &tr,
                                               ScanCount &cnt, const u32x4 *lds_root = nullptr, int root_mask = 0,
                                               int shift = 0)
 {
     const int base = tr.ni & ~3;
     u32x4 q0, q1, q2, q3;
+#if PTG_BVH_Q8
+    const SlabRay &r0 = r_in;
+    // 48-B node (bvh_build.hpp wide_q8) at byte 12 base: the words, the
+    // node's grid (binary16 origin in 256-step units, step exponents) and the
+    // 24 plane bytes, read as subnormal binary16 halves q 2^-24 by the box
+    // tests' v_fma_mix_f32: per axis t = h S + B with S = sx 2^(F + 8)
+    // (sx = 256 q_scale / d: sx 2^(E + 24)) and B = origin sx + bx
+    gptr<u32x4> qq = (gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + (unsigned)base * (PTG_BVH_Q8_STRIDE / 4u));
+    const u32x4 W = qq[0], Hd = qq[1], Pd = qq[2];
+    SlabRay r;
+    r.sx = __builtin_amdgcn_ldexpf(r0.sx, (int)__builtin_amdgcn_ubfe(Hd.y, 16, 5));
+    r.sy = __builtin_amdgcn_ldexpf(r0.sy, (int)__builtin_amdgcn_ubfe(Hd.y, 21, 5));
+    r.sz = __builtin_amdgcn_ldexpf(r0.sz, (int)__builtin_amdgcn_ubfe(Hd.y, 26, 5));
+    r.bx = __builtin_fmaf(lo_half(Hd.x), r0.sx, r0.bx);
+    r.by = __builtin_fmaf(hi_half(Hd.x), r0.sy, r0.by);
+    r.bz = __builtin_fmaf(lo_half(Hd.y), r0.sz, r0.bz);
+    // a dword's pairs: bytes (0, 2) and (1, 3) as the halves' low bytes
+    auto pe = [](unsigned d) { return d & 0x00FF00FFu; };
+    auto po = [](unsigned d) { return __builtin_amdgcn_perm(d, d, 0x0C030C01u); };
+    q0 = u32x4{pe(Hd.z), po(Hd.z), pe(Hd.w), W.x};
+    q1 = u32x4{po(Hd.w), pe(Pd.x), po(Pd.x), W.y};
+    q2 = u32x4{pe(Pd.y), po(Pd.y), pe(Pd.z), W.z};
+    q3 = u32x4{po(Pd.z), pe(Pd.w), po(Pd.w), W.w};
+    (void)lds_root;
+    (void)root_mask;
+    (void)shift;
+#else
+    const SlabRay &r = r_in;
 #if PTG_BVH_LDS_ROOT
     if (lds_root && (base & root_mask) == 0) {  // a layout's root: staged in LDS
         const u32x4 *l = lds_root + ((base >> shift) << 2);
@@ -1277,6 +1313,7 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
         q2 = q[2];
         q3 = q[3];
     }
+#endif
     if constexpr (kCount)
         cnt.boxes += 4 - (tr.ni & 3);
     const float tcap = tr.tb * 1.0001f;
@@ -3350,7 +3387,12 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t stride = PTG_BVH_WIDE && PTG_BVH_INTERLEAVE
                                   ? n_recs  // (interleaved: 8 x n_recs records in all, no layout stride)
                                   : (size_t(1) << shift) + (PTG_BVH_WIDE ? PTG_BVH_LAYOUT_PAD : 0);
+#if PTG_BVH_Q8
+        static_assert(PTG_BVH_WIDE && PTG_BVH_INTERLEAVE && !PTG_BVH_LDS_ROOT, "48-B nodes: the interleaved wide layouts");
+        const size_t off_cont = off_q + n_layouts * (stride / kWide) * PTG_BVH_Q8_STRIDE;
+#else
         const size_t off_cont = off_q + n_layouts * stride * sizeof(BvhNodeQ);
+#endif
         const size_t total = off_cont + (PTG_BVH_WIDE ? n_layouts * stride / kWide * sizeof(int32_t) : 0) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
@@ -3365,11 +3407,20 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
                 std::vector<BvhNodeQ> qk = wide_bvh(b, k, 0);
                 const std::vector<int32_t> ck = wide_conts(qk, 0);
                 for (size_t r = 0; r < qk.size(); ++r) {
-                    BvhNodeQ z = qk[r];
+                    BvhNodeQ &z = qk[r];
                     if (z.word >= 0)
                         z.word = ilv(z.word, k);
+#if !PTG_BVH_Q8
                     std::memcpy(blob.data() + off_q + (size_t)ilv((int32_t)r, k) * sizeof(BvhNodeQ), &z, sizeof(z));
+#endif
                 }
+#if PTG_BVH_Q8
+                // 48-B nodes: interleaved node 8 j + k at byte 48 (8 j + k)
+                for (size_t j = 0; j < qk.size() / kWide; ++j) {
+                    const WideQ8 w8 = wide_q8(&qk[j * kWide], k);
+                    std::memcpy(blob.data() + off_q + (j * 8 + (size_t)k) * PTG_BVH_Q8_STRIDE, &w8, sizeof(w8));
+                }
+#endif
                 for (size_t j = 0; j < ck.size(); ++j) {
                     const int32_t c = ck[j] >= 0 ? ilv(ck[j], k) : ck[j];
                     std::memcpy(blob.data() + off_cont + (j * 8 + (size_t)k) * sizeof(int32_t), &c, sizeof(c));
@@ -3404,7 +3455,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const WideGrid wg(b.nodes.empty() ? BvhNodeHost{} : b.nodes[0]);
         for (int c = 0; c < 3; ++c) {
             A.q_lo[c] = wg.centre[c];
-            A.q_scale[c] = wg.scale[c];
+            A.q_scale[c] = wg.scale[c] * (PTG_BVH_Q8 ? 256.0f : 1.0f);  // (48-B nodes: origins in 256-step units)
         }
         (void)grid;
 #else
