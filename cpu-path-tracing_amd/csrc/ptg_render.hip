@@ -1772,7 +1772,10 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // a wave with only mirror lanes skips the diffuse/dielectric work
     // (wave-uniform, exact: those lanes' values are all overwritten)
 #if PTG_DG_SKIP
-    if (__ballot(isD | isG) != 0ull)
+    // (the ballot of one compare, free from its lane mask: a ballot of
+    // isD | isG was materialised as v_cndmask + v_cmp; killed lanes of
+    // those materials run the block for nothing, their values unused)
+    if (__ballot(mat != PTG_SPECULAR) != 0ull)
 #endif
     {
         PTG_STAT(4);
