@@ -28,9 +28,9 @@ def func_lines(path):
     src = open(path).read().splitlines()
     marks = {}
     pats = {"camera_ray": r"void camera_ray\(", "scene_scan": r"const LinRec \*scene_scan\(",
-            "test_rec": r"auto test_rec = ", "test_end": r"auto test = \[&\]\(const int i", "box_mode": r"if \(PTG_ASSUME_BOX_MODE \|\| A\.box_mode\) \{", "axis_groups": r"\} else \{\s*$",
-            "scan_small": r"for \(; i < A\.n; \+\+i\)", "shade": r"^__device__ __forceinline__ bool shade\(const ShadeRec \*hit, float t, const float2 \*trig, f3 &o, f3 &d, f3 &T, f3 &E,$",
-            "dg_block": r"if \(__ballot\(isD \| isG\) != 0ull\)", "spec_block": r"if \(spec\) \{  // main.cpp:60",
+            "test_rec": r"auto test_geo = ", "test_end": r"auto test_rec = ", "box_mode": r"if \(PTG_ASSUME_BOX_MODE \|\| A\.box_mode\) \{", "axis_groups": r"\} else \{\s*$",
+            "box_end": r"i = \(PTG_WALLS_LAST && !kExact\) \? A\.n : A\.end_ax\[2\];", "shade": r"^__device__ __forceinline__ bool shade\(const ShadeRec \*hit, float t, const float2 \*trig, f3 &o, f3 &d, f3 &T, f3 &E,$",
+            "dg_block": r"if \(__ballot\(mat != PTG_SPECULAR\) != 0ull\)", "spec_block": r"if \(spec\) \{  // main.cpp:60",
             "ray_of": r"auto ray_of = ", "begin": r"auto begin = ", "flush": r"auto flush = ",
             "refill": r"auto refill = ", "main_loop": r"for \(;;\) \{"}
     for i, l in enumerate(src, 1):
@@ -55,7 +55,7 @@ def region_of(f, line, m):
         return "camera ray"
     if m["test_rec"] <= line < m["test_end"]:
         return "sphere test (test_rec)"
-    if m["box_mode"] <= line < m["scan_small"] - 5:
+    if m["box_mode"] <= line < m["box_end"]:
         return "box-mode walls"
     if m["scene_scan"] <= line < m["scene_scan"] + 200:
         return "scan control"
