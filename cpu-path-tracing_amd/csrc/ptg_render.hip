@@ -270,6 +270,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_D_INPLACE
 #define PTG_D_INPLACE 0  // shade: the next direction written into d in place (A/B)
 #endif
+#ifndef PTG_FAST_C_FOLD
+#define PTG_FAST_C_FOLD 1  // fast mode, small spheres: c = |e|^2 - R^2 with -R^2 folded into the first fma (box -0.8 %, box_mirror -0.9 %, quality rows unchanged; A/B r05zd)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -589,6 +592,13 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
         } else {
             hb = ed;
+#if PTG_FAST_C_FOLD
+            // fast mode: -R^2 folded into the first product of e.e (one add
+            // fewer; another rounding order of the same sum)
+            if constexpr (!kExact)
+                c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, g1.w)));
+            else
+#endif
             c = ee + g1.w;  // g1.w = -R^2
         }
         float disc;
