@@ -273,6 +273,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_FAST_C_FOLD
 #define PTG_FAST_C_FOLD 1  // fast mode, small spheres: c = |e|^2 - R^2 with -R^2 folded into the first fma (box -0.8 %, box_mirror -0.9 %, quality rows unchanged; A/B r05zd)
 #endif
+#ifndef PTG_FAST_C_FOLD_BVH
+#define PTG_FAST_C_FOLD_BVH 0  // the same for the BVH leaf spheres (A/B)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -995,6 +998,13 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
         c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
     } else {
         hb = ed;
+#if PTG_FAST_C_FOLD_BVH
+        // fast mode: -R^2 folded into the first fma of e.e (as scene_scan's
+        // small spheres, PTG_FAST_C_FOLD)
+        if constexpr (!kExact)
+            c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, g0.w)));
+        else
+#endif
         c = ee + g0.w;  // g0.w = -R^2
     }
     // the two culls and the discriminant test as one early-out (bitwise: the
