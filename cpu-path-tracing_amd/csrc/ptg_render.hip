@@ -276,6 +276,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_FAST_C_FOLD_BVH
 #define PTG_FAST_C_FOLD_BVH 0  // the same for the BVH leaf spheres (A/B)
 #endif
+#ifndef PTG_DRAW_MERGE
+#define PTG_DRAW_MERGE 1  // shade: every lane's first BRDF draw taken once before the samplers (exact; box -1.4 %, A/B r05zi)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -1781,6 +1784,16 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     const bool isD = !killed & (mat == PTG_DIFFUSE);
     const bool isG = !killed & (mat == PTG_DIELECTRIC);
     bool spec = !killed & (mat == PTG_SPECULAR);
+#if PTG_DRAW_MERGE
+    // every lane's first BRDF draw taken once, here: the diffuse phi, the
+    // dielectric's Fresnel draw -- or, where it cannot refract, its
+    // reflection's draw -- and the mirror's draw (main.cpp:46, :89, :62).
+    // A dielectric lane reflected by its Fresnel draw takes the reflection's
+    // draw below (fres).  Each lane's draws keep their order and count;
+    // killed lanes advance a state their ended path no longer reads.
+    const uint32_t m1 = draw_bits(st);
+    bool fres = false;
+#endif
 #if PTG_D_INPLACE
     // the next direction written into d in place: each lane's sampler writes
     // it after the lane's last read of d (a refraction only where no
@@ -1809,7 +1822,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         // and the refraction vector (wave-uniform, exact)
         if (__ballot(isG) == 0ull) {
             if (isD) {
+#if PTG_DRAW_MERGE
+                const uint32_t m_phi = m1;
+#else
                 const uint32_t m_phi = draw_bits(st);
+#endif
                 const float ra = draw(st);
                 float cp, sp;
                 Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
@@ -1835,7 +1852,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         float cp = 0.0f, sp = 0.0f, ra = 0.0f;
 #endif
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
+#if PTG_DRAW_MERGE
+            const uint32_t m_phi = m1;
+#else
             const uint32_t m_phi = draw_bits(st);
+#endif
             ra = draw(st);
             Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
         }
@@ -1857,7 +1878,12 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
                 float x2 = xm * xm;
                 float x5 = (x2 * x2) * xm;
                 float R = __builtin_fmaf(1.0f - r0, x5, r0);
+#if PTG_DRAW_MERGE
+                reflect = R > (float)m1 * 0x1p-24f;  // draw()'s value of m1
+                fres = true;
+#else
                 reflect = R > draw(st);
+#endif
             }
             spec = reflect;
         }
@@ -1892,7 +1918,15 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         PTG_STAT(5);
         float k = dot3(on, d);
         k = k + k;
+#if PTG_DRAW_MERGE
+        {  // the reflection's draw after a Fresnel draw (the others took m1)
+            uint32_t st2 = st;
+            (void)draw_bits(st2);
+            st = fres ? st2 : st;
+        }
+#else
         (void)draw(st);
+#endif
         nd = mk3(__builtin_fmaf(-k, on.x, d.x), __builtin_fmaf(-k, on.y, d.y), __builtin_fmaf(-k, on.z, d.z));
     }
     o = p;
