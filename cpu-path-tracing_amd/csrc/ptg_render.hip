@@ -279,6 +279,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_DRAW_MERGE
 #define PTG_DRAW_MERGE 1  // shade: every lane's first BRDF draw taken once before the samplers (exact; box -1.4 %, A/B r05zi)
 #endif
+#ifndef PTG_DRAW2_MERGE
+#define PTG_DRAW2_MERGE 0  // shade (with PTG_DRAW_MERGE): every lane's second BRDF draw taken once too (A/B)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -1793,6 +1796,14 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // killed lanes advance a state their ended path no longer reads.
     const uint32_t m1 = draw_bits(st);
     bool fres = false;
+#if PTG_DRAW2_MERGE
+    // and every lane's second draw, taken here too: the diffuse r, and the
+    // reflection's draw of a dielectric lane reflected by its Fresnel draw
+    // (its value unused, main.cpp:62); the state after it is kept only by
+    // those lanes (st2, committed after the samplers)
+    uint32_t st2 = st;
+    const uint32_t m2 = draw_bits(st2);
+#endif
 #endif
 #if PTG_D_INPLACE
     // the next direction written into d in place: each lane's sampler writes
@@ -1827,7 +1838,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #else
                 const uint32_t m_phi = draw_bits(st);
 #endif
+#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
+                const float ra = (float)m2 * 0x1p-24f;
+#else
                 const float ra = draw(st);
+#endif
                 float cp, sp;
                 Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
                 const f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
@@ -1857,7 +1872,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #else
             const uint32_t m_phi = draw_bits(st);
 #endif
+#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
+            ra = (float)m2 * 0x1p-24f;  // draw()'s value of m2
+#else
             ra = draw(st);
+#endif
             Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
         }
         // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
@@ -1918,7 +1937,9 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         PTG_STAT(5);
         float k = dot3(on, d);
         k = k + k;
-#if PTG_DRAW_MERGE
+#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
+        // (the reflection's draw after a Fresnel draw: st2, committed below)
+#elif PTG_DRAW_MERGE
         {  // the reflection's draw after a Fresnel draw (the others took m1)
             uint32_t st2 = st;
             (void)draw_bits(st2);
@@ -1929,6 +1950,9 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #endif
         nd = mk3(__builtin_fmaf(-k, on.x, d.x), __builtin_fmaf(-k, on.y, d.y), __builtin_fmaf(-k, on.z, d.z));
     }
+#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
+    st = (isD | (fres & spec)) ? st2 : st;
+#endif
     o = p;
     d = nd;
 #if !PTG_DEPTH_EARLY
