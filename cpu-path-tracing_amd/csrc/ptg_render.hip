@@ -282,6 +282,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_DRAW2_MERGE
 #define PTG_DRAW2_MERGE 0  // shade (with PTG_DRAW_MERGE): every lane's second BRDF draw taken once too (A/B)
 #endif
+#ifndef PTG_U1_HOIST
+#define PTG_U1_HOIST 1  // shade (with PTG_DRAW_MERGE): the first draw's value converted once (exact; A/B r05zl)
+#endif
+#ifndef PTG_CTH_MIN
+#define PTG_CTH_MIN 1  // shade, fast mode: cos theta clamped by v_min_f32 (with PTG_U1_HOIST box -0.45 %, box_mirror -0.25 %; A/B r05zl)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -1796,6 +1802,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // killed lanes advance a state their ended path no longer reads.
     const uint32_t m1 = draw_bits(st);
     bool fres = false;
+#if PTG_U1_HOIST
+    // its value u = m1 2^-24, converted once for the diffuse phi (fast
+    // mode: v_sin / v_cos take revolutions) and the Fresnel compare
+    const float u1 = (float)m1 * 0x1p-24f;
+#endif
 #if PTG_DRAW2_MERGE
     // and every lane's second draw, taken here too: the diffuse r, and the
     // reflection's draw of a dielectric lane reflected by its Fresnel draw
@@ -1877,6 +1888,12 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #else
             ra = draw(st);
 #endif
+#if PTG_U1_HOIST
+            if constexpr (!kExact) {
+                cp = __builtin_amdgcn_cosf(u1);  // Math<false>::sincos2pi of m1
+                sp = __builtin_amdgcn_sinf(u1);
+            } else
+#endif
             Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
         }
         // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
@@ -1885,7 +1902,12 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         const float r1 = Math<kExact>::rsqrt(dot3(v1, v1));
         v1 = mk3(v1.x * r1, v1.y * r1, v1.z * r1);
         const float x0 = -dot3(v1, nn);
+#if PTG_CTH_MIN
+        // fast mode: one v_min_f32 (differs from the select only for NaN)
+        const float cthG = kExact ? (1.0f < x0 ? 1.0f : x0) : __builtin_fminf(1.0f, x0);  // main.cpp:77
+#else
         const float cthG = 1.0f < x0 ? 1.0f : x0;  // main.cpp:77
+#endif
         // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
         const float s2 = Math<kExact>::sqrt0(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
         const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
@@ -1898,7 +1920,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
                 float x5 = (x2 * x2) * xm;
                 float R = __builtin_fmaf(1.0f - r0, x5, r0);
 #if PTG_DRAW_MERGE
+#if PTG_U1_HOIST
+                reflect = R > u1;
+#else
                 reflect = R > (float)m1 * 0x1p-24f;  // draw()'s value of m1
+#endif
                 fres = true;
 #else
                 reflect = R > draw(st);
