@@ -288,6 +288,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_CTH_MIN
 #define PTG_CTH_MIN 1  // shade, fast mode: cos theta clamped by v_min_f32 (with PTG_U1_HOIST box -0.45 %, box_mirror -0.25 %; A/B r05zl)
 #endif
+#ifndef PTG_FRES_IN_BLOCK
+#define PTG_FRES_IN_BLOCK 1  // shade: a Fresnel reflection's second draw taken in the Fresnel block, not the mirror block (exact; box_mirror -0.9 %, box +-0; A/B r05zm)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -1926,6 +1929,13 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
                 reflect = R > (float)m1 * 0x1p-24f;  // draw()'s value of m1
 #endif
                 fres = true;
+#if PTG_FRES_IN_BLOCK
+                {  // the reflection's draw right after the Fresnel draw that chose it
+                    uint32_t st2 = st;
+                    (void)draw_bits(st2);
+                    st = reflect ? st2 : st;
+                }
+#endif
 #else
                 reflect = R > draw(st);
 #endif
@@ -1965,6 +1975,8 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         k = k + k;
 #if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
         // (the reflection's draw after a Fresnel draw: st2, committed below)
+#elif PTG_DRAW_MERGE && PTG_FRES_IN_BLOCK
+        // (the reflection's draw after a Fresnel draw: taken in the Fresnel block)
 #elif PTG_DRAW_MERGE
         {  // the reflection's draw after a Fresnel draw (the others took m1)
             uint32_t st2 = st;
