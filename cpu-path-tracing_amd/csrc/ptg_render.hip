@@ -291,6 +291,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_FRES_IN_BLOCK
 #define PTG_FRES_IN_BLOCK 1  // shade: a Fresnel reflection's second draw taken in the Fresnel block, not the mirror block (exact; box_mirror -0.9 %, box +-0; A/B r05zm)
 #endif
+#ifndef PTG_XWALL_GEO
+#define PTG_XWALL_GEO 1  // box mode's extra walls from the wall geometry table (one LDS read per pass instead of two; exact; box_mirror -0.6 %, A/B r05zn)
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -764,7 +767,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // only from beyond its tangent plane (below).
         // wall table after the sentinel: byte offsets of the records of axis
         // k's + wall (2k) and - wall (2k + 1), -1 where missing
-        const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
+        [[maybe_unused]] const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
         float u[3], v[3];
 #if PTG_KN_MASKS
         bool posk[3];
@@ -926,9 +929,20 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 m &= m - 1u;
                 const int k = j < 3 ? j : (j < 6 ? j - 3 : 0);
                 const bool toward = j < 3;
+#if PTG_XWALL_GEO && PTG_WALL_GEO
+                // the wall's geometry entry (axis, side) of the table above:
+                // one dependent LDS read; a missing wall's NaN geometry never
+                // passes the cull's compares' win
+                const int side = (comp(d, k) >= 0.0f) == toward ? 0 : 1;
+                const GeoRec &gx = reinterpret_cast<const GeoRec *>(recs + A.n + 2)[2 * k + side];
+                const float4 x0 = gx.g0, x1 = gx.g1;
+                test_geo(rec_at(__float_as_int(x1.x)), x0, x1, std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
+                         j < 6, k);
+#else
                 const int off = walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)];
                 test_rec(rec_at(off >= 0 ? off : 0), std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
                          (j < 6) & (off >= 0), k);
+#endif
             }
 #else
             auto wall = [&](int k, bool toward) {
