@@ -1818,7 +1818,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // draw below (fres).  Each lane's draws keep their order and count;
     // killed lanes advance a state their ended path no longer reads.
     const uint32_t m1 = draw_bits(st);
-    bool fres = false;
+    [[maybe_unused]] bool fres = false;
 #if PTG_U1_HOIST
     // its value u = m1 2^-24, converted once for the diffuse phi (fast
     // mode: v_sin / v_cos take revolutions) and the Fresnel compare
