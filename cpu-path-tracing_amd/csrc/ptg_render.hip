@@ -294,6 +294,21 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_XWALL_GEO
 #define PTG_XWALL_GEO 1  // box mode's extra walls from the wall geometry table (one LDS read per pass instead of two; exact; box_mirror -0.6 %, A/B r05zn)
 #endif
+#ifndef PTG_BEST_IDX
+// linear scan: the winner kept as a record index relative to the sentinel
+// (the three small spheres -3, -2, -1: inline constants, no v_mov per
+// select; the wall table holds the walls' relative indices), the record
+// address formed once after the scan (exact: bookkeeping only; with
+// PTG_FAST_NO_DISC box -0.2 %, box_mirror -0.5 %, A/B r05zs)
+#define PTG_BEST_IDX 1
+#endif
+#ifndef PTG_FAST_NO_DISC
+// fast mode: no disc < 0 compare in the candidate test -- v_sqrt_f32 of a
+// negative is NaN, so qq and den are NaN and the cross-multiplied compare
+// fails (exact: the same decisions; the exact mode's Goldschmidt sqrt is
+// finite there and keeps the compare; A/B r05zs)
+#define PTG_FAST_NO_DISC 1
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -566,8 +581,14 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     // compared by cross-multiplication, only the winner is divided
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
+#if PTG_BEST_IDX
+    int bi = 0;  // the winner: recs + A.n + bi (0: the sentinel, no hit)
+    auto ri_of = [&](const LinRec *r) { return (int)(r - recs) - A.n; };
+#else
     const LinRec *best = recs + A.n;
-    auto test_geo = [&](const LinRec *r, const float4 g0, const float4 g1, auto kind_tag, const float un = 0.0f,
+#endif
+    // r: the record (PTG_BEST_IDX: its index relative to the sentinel)
+    auto test_geo = [&](const auto r, const float4 g0, const float4 g1, auto kind_tag, const float un = 0.0f,
                         const float vn = 0.0f, const bool valid = true, const int ks = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
         // r is wave-uniform, except for a pair's walls / box mode
@@ -682,16 +703,25 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         }
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
-        bool win = valid & !(disc < 0.0f) & !(num < kEps * den) & (num * bq < bn * den);
+        bool win = valid & ((PTG_FAST_NO_DISC && !kExact) || !(disc < 0.0f)) & !(num < kEps * den) &
+                   (num * bq < bn * den);
         if constexpr (kKind == kAxAnyOut)
             win = win & neg;
         bn = win ? num : bn;
         bq = win ? den : bq;
+#if PTG_BEST_IDX
+        bi = win ? r : bi;
+#else
         best = win ? r : best;
+#endif
     };
     auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
                         const bool valid = true, const int ks = 0) {
+#if PTG_BEST_IDX
+        test_geo(ri_of(r), r->g.g0, r->g.g1, kind_tag, un, vn, valid, ks);
+#else
         test_geo(r, r->g.g0, r->g.g1, kind_tag, un, vn, valid, ks);
+#endif
     };
     auto test = [&](const int i, auto kind_tag) { test_rec(recs + i, kind_tag); };
     // scan order: axis-anchored walls (x, y, z), general huge spheres, small
@@ -741,10 +771,18 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // each record's geometry read one test ahead (its LDS latency
             // behind the previous test; the first at the scan's start)
             const float4 a1 = r0[1].g.g0, b1 = r0[1].g.g1;
+#if PTG_BEST_IDX
+            // (i = A.n - 3 here: the relative indices are constants)
+            test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
+            const float4 a2 = r0[2].g.g0, b2 = r0[2].g.g1;
+            test_geo(-2, a1, b1, std::integral_constant<int, kSmall>{});
+            test_geo(-1, a2, b2, std::integral_constant<int, kSmall>{});
+#else
             test_geo(r0, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
             const float4 a2 = r0[2].g.g0, b2 = r0[2].g.g1;
             test_geo(r0 + 1, a1, b1, std::integral_constant<int, kSmall>{});
             test_geo(r0 + 2, a2, b2, std::integral_constant<int, kSmall>{});
+#endif
 #else
             test_rec(r0, std::integral_constant<int, kSmall>{});
             test_rec(r0 + 1, std::integral_constant<int, kSmall>{});
@@ -825,7 +863,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls + 2 * kn) +
                                                       (comp(d, kn) >= 0.0f ? 0 : 4));
 #endif
-        auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
+        [[maybe_unused]] auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
 #if PTG_INROOM_EARLY
@@ -845,7 +883,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                       (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
             __builtin_amdgcn_sched_barrier(0);
 #endif
+#if PTG_BEST_IDX
+            test_geo(__float_as_int(g1.x), g0, g1,
+#else
             test_geo(rec_at(__float_as_int(g1.x)), g0, g1,
+#endif
                      std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{}, un, vn);
         }
 #else
@@ -936,7 +978,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 const int side = (comp(d, k) >= 0.0f) == toward ? 0 : 1;
                 const GeoRec &gx = reinterpret_cast<const GeoRec *>(recs + A.n + 2)[2 * k + side];
                 const float4 x0 = gx.g0, x1 = gx.g1;
+#if PTG_BEST_IDX
+                test_geo(__float_as_int(x1.x), x0, x1, std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
+#else
                 test_geo(rec_at(__float_as_int(x1.x)), x0, x1, std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
+#endif
                          j < 6, k);
 #else
                 const int off = walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)];
@@ -990,8 +1036,13 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
     small_spheres(i);
+#if PTG_BEST_IDX
+    tbest = bi != 0 ? Math<kExact>::div(bn, bq) : kInf;
+    return recs + A.n + bi;
+#else
     tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
     return best;
+#endif
 }
 
 // Scenes with more than kLinearMax spheres: the huge
@@ -3414,7 +3465,9 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             const int off = walls[e];
             if (order.box_mode && off >= 0 && off / (int)sizeof(LinRec) < (int)n_spheres) {
                 wg[e] = lgeo[off / (int)sizeof(LinRec)];
-                std::memcpy(&wg[e].g1.x, &off, 4);
+                // the record's byte offset (PTG_BEST_IDX: its index relative to the sentinel)
+                const int32_t tag = PTG_BEST_IDX ? off / (int)sizeof(LinRec) - (int)n_spheres : off;
+                std::memcpy(&wg[e].g1.x, &tag, 4);
             } else {
                 wg[e].g0 = make_float4(qnan, qnan, qnan, qnan);
                 wg[e].g1 = make_float4(0.0f, qnan, qnan, qnan);
