@@ -67,7 +67,7 @@ inline double half_area(const double mn[3], const double mx[3])
 #endif
 constexpr int kSahBins = PTG_SAH_BINS;
 inline int sah_split(const ptg_sphere *s, std::vector<int32_t> &idx, int lo, int hi, const double cmn[3],
-                     const double cmx[3], int &axis)
+                     const double cmx[3], int &axis, double *cost_out = nullptr)
 {
     double best = INFINITY;
     int best_axis = -1, best_bin = -1;
@@ -124,6 +124,8 @@ inline int sah_split(const ptg_sphere *s, std::vector<int32_t> &idx, int lo, int
             }
         }
     }
+    if (cost_out)
+        *cost_out = best;
     if (best_axis < 0)
         return -1;
     axis = best_axis;
@@ -158,7 +160,23 @@ inline int build_rec(const ptg_sphere *s, std::vector<int32_t> &idx, int lo, int
             n.bmax[c] = widen_up(mx[c], pad);
         }
     }
+#ifndef PTG_SAH_LEAF_CT
+#define PTG_SAH_LEAF_CT 0  // > 0: a group of <= kLeafSize spheres is split too where the SAH says so (box test cost in sphere tests x 10; A/B)
+#endif
+    int mid = -1, axis = 0;
+#if PTG_SAH_LEAF_CT > 0
+    if (hi - lo <= kLeafSize && hi - lo >= 2) {
+        double cost = INFINITY;
+        const int m = sah_split(s, idx, lo, hi, cmn, cmx, axis, &cost);
+        // split cost: two box tests more (the children's) + the children's
+        // spheres weighted by their area, against every sphere of the leaf
+        if (m > lo && m < hi && 0.2 * PTG_SAH_LEAF_CT * half_area(mn, mx) + cost < (hi - lo) * half_area(mn, mx))
+            mid = m;
+    }
+    if (mid < 0 && hi - lo <= kLeafSize) {
+#else
     if (hi - lo <= kLeafSize) {
+#endif
         const int first = (int)b.order.size();
         for (int i = lo; i < hi; ++i)
             b.order.push_back(idx[i]);
@@ -166,14 +184,15 @@ inline int build_rec(const ptg_sphere *s, std::vector<int32_t> &idx, int lo, int
         b.nodes[me].skip = me + 1;
         return me;
     }
-    int axis = 0;
-    for (int c = 1; c < 3; ++c)
-        if (cmx[c] - cmn[c] > cmx[axis] - cmn[axis])
-            axis = c;
-    int mid = -1;
+    if (mid < 0) {
+        axis = 0;
+        for (int c = 1; c < 3; ++c)
+            if (cmx[c] - cmn[c] > cmx[axis] - cmn[axis])
+                axis = c;
 #if PTG_BVH_SAH
-    mid = sah_split(s, idx, lo, hi, cmn, cmx, axis);
+        mid = sah_split(s, idx, lo, hi, cmn, cmx, axis);
 #endif
+    }
     if (mid < 0) {  // median split along the longest centroid axis
         mid = (lo + hi) / 2;
         std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi, [&](int32_t a, int32_t c) {
