@@ -255,6 +255,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_WALLS_LAST
 #define PTG_WALLS_LAST 0  // fast box mode: the small spheres tested before the extra walls (A/B)
 #endif
+#ifndef PTG_SMALL_FIRST
+// fast box mode: the small spheres tested between the nearest wall's LDS read
+// and its test (the read's latency behind their work; only exact ties
+// between a wall and a small sphere can resolve differently; A/B)
+#define PTG_SMALL_FIRST 0
+#endif
 #ifndef PTG_SMALL_PREFETCH
 #define PTG_SMALL_PREFETCH 1  // the three small spheres' records read one test ahead, the first at the scan's start (box -0.2 %, box_mirror -0.3 %, A/B r05t)
 #endif
@@ -308,6 +314,13 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // fails (exact: the same decisions; the exact mode's Goldschmidt sqrt is
 // finite there and keeps the compare; A/B r05zs)
 #define PTG_FAST_NO_DISC 1
+#endif
+#ifndef PTG_FAST_NN
+// shade, fast mode: the facing normal as (p - C) (+-1/R) with the side from
+// (p - C).d (one select instead of three), the mirror's n.d from that dot
+// (one mul instead of a dot product); another rounding of the same values
+// (box -0.2 %, box_mirror -0.2 %, A/B r05zz)
+#define PTG_FAST_NN 1
 #endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
@@ -875,6 +888,12 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             const GeoRec *wg = reinterpret_cast<const GeoRec *>(recs + A.n + 2);
             const GeoRec &g = *reinterpret_cast<const GeoRec *>(reinterpret_cast<const char *>(wg) + 8 * offn);
             const float4 g0 = g.g0, g1 = g.g1;
+#if PTG_SMALL_FIRST
+            if constexpr (!kExact) {
+                int j = A.end_ax[2];
+                small_spheres(j);
+            }
+#endif
 #if PTG_INROOM_EARLY
             // (independent of the wall test: its compares issued while the
             // wall record's LDS read is in flight -- held there by a
@@ -1027,7 +1046,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             }
 #endif
         }
-        i = (PTG_WALLS_LAST && !kExact) ? A.n : A.end_ax[2];
+        i = ((PTG_WALLS_LAST || PTG_SMALL_FIRST) && !kExact) ? A.n : A.end_ax[2];
     } else {
         axis_group(std::integral_constant<int, kAxX>{});
         axis_group(std::integral_constant<int, kAxY>{});
@@ -1823,9 +1842,22 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
     // hit_record.cpp:6 (p - C).norm() as (p - C) * (1/R): p lies on the sphere
     const float invR = S.s2.w;
-    f3 on = mk3((p.x - s0.x) * invR, (p.y - s0.y) * invR, (p.z - s0.z) * invR);
-    bool front = dot3(on, d) < 0.0f;
-    f3 nn = front ? on : mk3(-on.x, -on.y, -on.z);
+    bool front;
+    f3 on, nn;
+    [[maybe_unused]] float kn = 0.0f;  // PTG_FAST_NN: nn.d
+    if (PTG_FAST_NN && !kExact) {
+        const f3 pc = mk3(p.x - s0.x, p.y - s0.y, p.z - s0.z);
+        const float sd = dot3(pc, d);
+        front = sd < 0.0f;
+        const float ks = front ? invR : -invR;
+        nn = mk3(pc.x * ks, pc.y * ks, pc.z * ks);
+        kn = sd * ks;
+        on = nn;  // (unused: the mirror reflects on nn)
+    } else {
+        on = mk3((p.x - s0.x) * invR, (p.y - s0.y) * invR, (p.z - s0.z) * invR);
+        front = dot3(on, d) < 0.0f;
+        nn = front ? on : mk3(-on.x, -on.y, -on.z);
+    }
     // main.cpp:126
     E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
     // main.cpp:128-139: Russian roulette after depth 4.  Both colour records
@@ -2036,7 +2068,8 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     }
     if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
         PTG_STAT(5);
-        float k = dot3(on, d);
+        // (PTG_FAST_NN: on the facing normal nn = +-on, its dot kn)
+        float k = (PTG_FAST_NN && !kExact) ? kn : dot3(on, d);
         k = k + k;
 #if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
         // (the reflection's draw after a Fresnel draw: st2, committed below)
@@ -2051,7 +2084,8 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
 #else
         (void)draw(st);
 #endif
-        nd = mk3(__builtin_fmaf(-k, on.x, d.x), __builtin_fmaf(-k, on.y, d.y), __builtin_fmaf(-k, on.z, d.z));
+        const f3 rn = (PTG_FAST_NN && !kExact) ? nn : on;
+        nd = mk3(__builtin_fmaf(-k, rn.x, d.x), __builtin_fmaf(-k, rn.y, d.y), __builtin_fmaf(-k, rn.z, d.z));
     }
 #if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
     st = (isD | (fres & spec)) ? st2 : st;
