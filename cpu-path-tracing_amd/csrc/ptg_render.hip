@@ -322,6 +322,15 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // (box -0.2 %, box_mirror -0.2 %, A/B r05zz)
 #define PTG_FAST_NN 1
 #endif
+#ifndef PTG_BEST_LEAF
+// BVH scan: the winner kept as its leaf-order index (huge sphere k: -2 - k)
+// and turned into its scene index once, when the scan ends -- no dependent
+// scene-index load per winning candidate in the leaf loop; an exact tie of t
+// reads both scene indices (the lex rule, the same winner; A/B r05zza: C5
+// +5.3 % -- the one load at the scan's end sits right before shading, while
+// the leaf loop's loads were hidden)
+#define PTG_BEST_LEAF 0
+#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -1169,6 +1178,23 @@ __device__ __forceinline__ void update_lex(const float t, const int sid, float &
 // SGPRs lose their address space, and generic (flat) loads also wait on LDS
 template <class T>
 using gptr = const T __attribute__((address_space(1))) *;
+#if PTG_BEST_LEAF
+// PTG_BEST_LEAF: a winner code -> its scene index (-1: none)
+__device__ __forceinline__ int sid_of(const KArgs &A, const int c)
+{
+    return c >= 0 ? ((gptr<int>)A.bvh_id)[c] : (c == -1 ? -1 : ((gptr<int>)A.big_id)[-2 - c]);
+}
+// update_lex on winner codes: a nearer t wins; an exact tie reads both scene
+// indices (rare) and the lower wins, as update_lex
+__device__ __forceinline__ void update_lex_c(const KArgs &A, const float t, const int c, float &tb, int &best)
+{
+    bool win = t < tb;
+    if (t == tb)
+        win = (unsigned)sid_of(A, c) < (unsigned)sid_of(A, best);
+    tb = win ? t : tb;
+    best = win ? c : best;
+}
+#endif
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // a compact node record, loadable from gptr
 
 struct BvhTrav {
@@ -1229,8 +1255,13 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.tb = kInf;
     tr.best = -1;
     for (int k = 0; k < A.n_big; ++k)
+#if PTG_BEST_LEAF
+        update_lex_c(A, root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb, tr.tb * kCullScale),
+                     -2 - k, tr.tb, tr.best);
+#else
         update_lex(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb, tr.tb * kCullScale),
                    A.big_id[k], tr.tb, tr.best);
+#endif
     if constexpr (kCount)
         cnt.spheres += A.n_big;
 #if PTG_BVH_WIDE
@@ -1618,7 +1649,12 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
 #endif
         const float t = root_lex<false, kExact>(rec, float4{}, o, d, a, tb, tbm);
         if (t <= tb) {  // the scene index is read only for a candidate that wins or ties
+#if PTG_BEST_LEAF
+            (void)ids;
+            update_lex_c(A, t, f + j, tb, best);
+#else
             update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
+#endif
             tbm = tb * kCullScale;
         }
     }
@@ -1749,8 +1785,13 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     const float htb = bpf(partner, tb), htb2 = bpf(partner2, tb);
     const int hbest = bpi(partner, best), hbest2 = bpi(partner2, best);
     if (po) {
+#if PTG_BEST_LEAF
+        update_lex_c(A, htb, hbest, tb, best);
+        update_lex_c(A, htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
+#else
         update_lex(htb, hbest, tb, best);
         update_lex(htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
+#endif
     }
 #if PTG_BVH_WIDE && PTG_LEAF_DONE_SEL
     tr.tb = has ? tb : tr.tb;
@@ -1780,7 +1821,11 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
             bvh_node_step<kCount>((gptr<int>)A.bvh_cont, (gptr<u32x4>)A.bvh_qnodes, sr, tr, cnt);
     }
     tbest = tr.tb;
+#if PTG_BEST_LEAF
+    return sid_of(A, tr.best);
+#else
     return tr.best;
+#endif
 }
 
 // Per-lane state machine: one call = one bounce segment of radiance()
@@ -2617,7 +2662,12 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             PTG_PHASE(5);
             if (item >= 0 && phase == 2) {
                 phase = 0;
-                if (shade<kExact>(tr.best >= 0 ? A.shade + tr.best : nullptr, tr.tb, trig, o, d, T, E, depth, st))
+#if PTG_BEST_LEAF
+                const int sid = sid_of(A, tr.best);
+#else
+                const int sid = tr.best;
+#endif
+                if (shade<kExact>(sid >= 0 ? A.shade + sid : nullptr, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
             PTG_PHASE(3);
