@@ -322,6 +322,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // (box -0.2 %, box_mirror -0.2 %, A/B r05zz)
 #define PTG_FAST_NN 1
 #endif
+#ifndef PTG_RR_ROWSEL
+// shade: the roulette's colour row (s2, or s3 = s2 / p past the roulette
+// depth) selected by address -- one record read, no selects; 1/R is in both
+// rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
+#define PTG_RR_ROWSEL 1
+#endif
 #ifndef PTG_BEST_LEAF
 // BVH scan: the winner kept as its leaf-order index (huge sphere k: -2 - k)
 // and turned into its scene index once, when the scan ends -- no dependent
@@ -1886,7 +1892,13 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // hit_record.cpp:3-12
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
     // hit_record.cpp:6 (p - C).norm() as (p - C) * (1/R): p lies on the sphere
+#if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
+    const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
+    const float4 cc = *(rr ? &S.s3 : &S.s2);  // (prepare_scene: 1/R in s2.w and s3.w)
+    const float invR = cc.w;
+#else
     const float invR = S.s2.w;
+#endif
     bool front;
     f3 on, nn;
     [[maybe_unused]] float kn = 0.0f;  // PTG_FAST_NN: nn.d
@@ -1905,12 +1917,15 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     }
     // main.cpp:126
     E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
-    // main.cpp:128-139: Russian roulette after depth 4.  Both colour records
-    // are loaded and selected (3 selects instead of address arithmetic)
-#if !PTG_SHADE_EARLY
+    // main.cpp:128-139: Russian roulette after depth 4 (PTG_RR_ROWSEL: the
+    // colour row read above by address; else both rows read and selected)
+#if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
+#elif !PTG_SHADE_EARLY
     const float4 c2 = S.s2, c3 = S.s3;
-#endif
     const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
+#else
+    const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
+#endif
     // Russian roulette without an early return: the roulette's draw advances the state of the
     // rr lanes only (a select), and a killed lane runs on with its materials
     // masked -- its next ray and state are discarded (the early return's
@@ -1929,7 +1944,11 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     st = rr ? st_rr : st;
     const bool killed = rr & !(u_rr < s0.w);  // (box -0.6 %, box_mirror -1.0 %)
 #endif
+#if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
+    T = mk3(T.x * cc.x, T.y * cc.y, T.z * cc.z);
+#else
     T = mk3(T.x * (rr ? c3.x : c2.x), T.y * (rr ? c3.y : c2.y), T.z * (rr ? c3.z : c2.z));
+#endif
     // BRDF samplers (main.cpp:44-97).  Diffuse and dielectric lanes share the
     // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
     // holding both materials issues them once; every lane's arithmetic is the
@@ -3027,7 +3046,7 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
 #endif
         r.s1 = make_float4((float)sp.emission[0], (float)sp.emission[1], (float)sp.emission[2], matf);
         r.s2 = make_float4(cx, cy, cz, (float)(1.0 / R));
-        r.s3 = make_float4(rx, ry, rz, 0.0f);
+        r.s3 = make_float4(rx, ry, rz, PTG_RR_ROWSEL ? (float)(1.0 / R) : 0.0f);
         shade[i] = r;
     }
 }
