@@ -328,6 +328,14 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_SHADE_LEAF
+// (with PTG_BEST_LEAF) the shading records also in leaf order (the huge
+// spheres before them), addressed by the winner's code directly: no scene
+// index is read to shade (A/B r05zze: C5 +4.5 % with PTG_BEST_LEAF, which
+// alone costs +5.9 % there -- the codes' tie branch in the leaf loop, not
+// the index load, is the cost)
+#define PTG_SHADE_LEAF 0
+#endif
 #ifndef PTG_BEST_LEAF
 // BVH scan: the winner kept as its leaf-order index (huge sphere k: -2 - k)
 // and turned into its scene index once, when the scan ends -- no dependent
@@ -365,6 +373,7 @@ inline bool is_huge(const ptg_sphere &sp, const ptg_camera *cam)
 struct KArgs {
     const LinRec *lin;      // linear scenes (<= kLinearMax): n records in scan order + sentinel
     const ShadeRec *shade;  // BVH scenes: shading records in scene index order
+    const ShadeRec *shade_leaf;  // PTG_SHADE_LEAF: the same by winner code (leaf j at [j], huge sphere k at [-2 - k])
     int n;
     // linear scenes: records in SCAN order (prepare_scan_order), grouped by
     // kind: [0, end_ax[0]) huge spheres anchored on the x axis, then y, then z
@@ -2681,12 +2690,16 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             PTG_PHASE(5);
             if (item >= 0 && phase == 2) {
                 phase = 0;
-#if PTG_BEST_LEAF
+#if PTG_BEST_LEAF && PTG_SHADE_LEAF
+                const ShadeRec *hrec = tr.best != -1 ? A.shade_leaf + tr.best : nullptr;
+#elif PTG_BEST_LEAF
                 const int sid = sid_of(A, tr.best);
+                const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
 #else
                 const int sid = tr.best;
+                const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
 #endif
-                if (shade<kExact>(sid >= 0 ? A.shade + sid : nullptr, tr.tb, trig, o, d, T, E, depth, st))
+                if (shade<kExact>(hrec, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
             PTG_PHASE(3);
@@ -2905,6 +2918,7 @@ struct ptg_context {
     int wave_slots;     // CUs x 32 resident waves (split-tail sizing)
     LinRec *d_lin;      // linear scenes
     ShadeRec *d_shade;  // BVH scenes
+    ShadeRec *d_shade_leaf = nullptr;  // PTG_SHADE_LEAF
     void *d_bvh;  // one allocation: nodes | leaf geometry | leaf ids | big geometry | big ids
     float2 *d_trig;  // sin/cos table (trig_table)
     unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
@@ -3779,6 +3793,23 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         A.big_id = reinterpret_cast<const int *>(base + off_bid);
         A.n_nodes = (int)n_recs;
         A.n_big = (int)n_big;
+#if PTG_SHADE_LEAF
+        {
+            // [n_big - 1 - k]: huge sphere k (code -2 - k); [n_big]: unused
+            // (code -1); [n_big + 1 + j]: leaf sphere j (code j)
+            std::vector<ShadeRec> sl(n_big + 1 + n_leaf);
+            for (size_t k = 0; k < n_big; ++k)
+                sl[n_big - 1 - k] = shade[b.big[k]];
+            for (size_t j = 0; j < n_leaf; ++j)
+                sl[n_big + 1 + j] = shade[b.order[j]];
+            if (hipMalloc(&ctx->d_shade_leaf, sl.size() * sizeof(ShadeRec)) != hipSuccess) {
+                ptg_context_destroy(ctx);
+                return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the leaf-order shading records failed");
+            }
+            PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade_leaf, sl.data(), sl.size() * sizeof(ShadeRec), hipMemcpyHostToDevice));
+            A.shade_leaf = ctx->d_shade_leaf + n_big + 1;
+        }
+#endif
     }
     A.pos_x = (float)cam->position[0];
     A.pos_y = (float)cam->position[1];
@@ -3832,6 +3863,8 @@ int ptg_context_destroy(ptg_context *ctx)
         (void)hipFree(ctx->d_lin);
     if (ctx->d_shade)
         (void)hipFree(ctx->d_shade);
+    if (ctx->d_shade_leaf)
+        (void)hipFree(ctx->d_shade_leaf);
     if (ctx->d_trig)
         (void)hipFree(ctx->d_trig);
     if (ctx->d_bvh)
