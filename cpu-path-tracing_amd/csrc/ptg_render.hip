@@ -328,6 +328,11 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_LEAF_NOBRANCH
+// BVH leaf loop: every candidate's scene index loaded and the lex update as
+// selects, no branch on t <= tb (A/B r05zzf: C5 +2.6 %)
+#define PTG_LEAF_NOBRANCH 0
+#endif
 #ifndef PTG_SHADE_LEAF
 // (with PTG_BEST_LEAF) the shading records also in leaf order (the huge
 // spheres before them), addressed by the winner's code directly: no scene
@@ -1663,7 +1668,13 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
         const float4 rec = *(const float4 *)(sph + off);
 #endif
         const float t = root_lex<false, kExact>(rec, float4{}, o, d, a, tb, tbm);
+#if PTG_LEAF_NOBRANCH && !PTG_BEST_LEAF
+        update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
+        tbm = tb * kCullScale;
+        if (false) {
+#else
         if (t <= tb) {  // the scene index is read only for a candidate that wins or ties
+#endif
 #if PTG_BEST_LEAF
             (void)ids;
             update_lex_c(A, t, f + j, tb, best);
