@@ -328,6 +328,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_SMALL_G0W
+// linear scan: a small sphere's -R^2 also in g0.w (prepare_scene), so its
+// test reads one 16-B word of its record (ds_read_b128) instead of g0.xyz
+// and g1.w (exact; box -0.3 %, box_mirror -0.2 %, A/B r05zzg)
+#define PTG_SMALL_G0W 1
+#endif
 #ifndef PTG_LEAF_NOBRANCH
 // BVH leaf loop: every candidate's scene index loaded and the lex update as
 // selects, no branch on t <= tb (A/B r05zzf: C5 +2.6 %)
@@ -680,10 +686,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // fast mode: -R^2 folded into the first product of e.e (one add
             // fewer; another rounding order of the same sum)
             if constexpr (!kExact)
-                c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, g1.w)));
+                c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, PTG_SMALL_G0W ? g0.w : g1.w)));
             else
 #endif
-            c = ee + g1.w;  // g1.w = -R^2
+            c = ee + (PTG_SMALL_G0W ? g0.w : g1.w);  // g1.w = -R^2 (PTG_SMALL_G0W: g0.w too)
         }
         float disc;
         if constexpr (kKind == kSmall) {
@@ -695,7 +701,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // 5e-5).  Huge spheres keep hb^2 - a c: there the anchored hb, c
             // are accurate and a R^2 would be ~1e12.
             const f3 x = cross3(e, d);
-            disc = __builtin_fmaf(a, -g1.w, -dot3(x, x));
+            disc = __builtin_fmaf(a, -(PTG_SMALL_G0W ? g0.w : g1.w), -dot3(x, x));
         } else {
             disc = __builtin_fmaf(hb, hb, -(a * c));
         }
@@ -3038,7 +3044,8 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
             g.g0 = make_float4((float)P[0], (float)P[1], (float)P[2], (float)R);
             g.g1 = make_float4((float)N[0], (float)N[1], (float)N[2], (float)(2.0 * R));
         } else {
-            g.g0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], -1.0f);
+            g.g0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2],
+                               PTG_SMALL_G0W ? (float)(-(R * R)) : -1.0f);
             g.g1 = make_float4(0.0f, 0.0f, 0.0f, (float)(-(R * R)));
         }
         geo[i] = g;
