@@ -328,6 +328,13 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_BIG_SCALAR
+// BVH scan: the huge spheres' records (wave-uniform addresses) read through
+// the constant address space -- scalar loads, not 64-lane vector loads whose
+// data the texture data path (TD, 94 % busy on C5) returns to every lane
+// (C5 -0.3 %, A/B r05zzj)
+#define PTG_BIG_SCALAR 1
+#endif
 #ifndef PTG_SMALL_G0W
 // linear scan: a small sphere's -R^2 also in g0.w (prepare_scene), so its
 // test reads one 16-B word of its record (ds_read_b128) instead of g0.xyz
@@ -1280,6 +1287,19 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     const float a = dot3(d, d);
     tr.tb = kInf;
     tr.best = -1;
+#if PTG_BIG_SCALAR
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(4))) f32x4 *cvec_t;
+    typedef const __attribute__((address_space(4))) int *cint_t;
+    const cvec_t bgeo = (cvec_t)A.big_geo;  // GeoRec k: words 2 k, 2 k + 1
+    const cint_t bid = (cint_t)A.big_id;
+    for (int k = 0; k < A.n_big; ++k) {
+        const f32x4 v0 = bgeo[2 * k], v1 = bgeo[2 * k + 1];
+        const float4 g0 = make_float4(v0.x, v0.y, v0.z, v0.w), g1 = make_float4(v1.x, v1.y, v1.z, v1.w);
+        update_lex(root_lex<true, kExact>(g0, g1, o, d, a, tr.tb, tr.tb * kCullScale), bid[k], tr.tb, tr.best);
+    }
+    if (false)
+#endif
     for (int k = 0; k < A.n_big; ++k)
 #if PTG_BEST_LEAF
         update_lex_c(A, root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb, tr.tb * kCullScale),
