@@ -328,6 +328,13 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_SHADE_PACK
+// BVH scenes: the shading record's material and an emission flag packed into
+// s0.w beside the roulette threshold (bits 28-29, 30), s1 (the emission) read
+// only by lanes that hit an emitter -- two 16-B global loads per hit instead
+// of three (exact: the same values; A/B r05zzl: C5 +-0)
+#define PTG_SHADE_PACK 0
+#endif
 #ifndef PTG_BIG_SCALAR
 // BVH scan: the huge spheres' records (wave-uniform addresses) read through
 // the constant address space -- scalar loads, not 64-lane vector loads whose
@@ -1885,7 +1892,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
 // its radiance.
 // shade(): everything after the scene scan -- sky on a miss, else hit
 // record, emission, Russian roulette, BRDF sampling of the next ray.
-template <bool kExact>
+template <bool kExact, bool kPacked = false>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st);
 
@@ -1902,10 +1909,10 @@ __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, cons
         const LinRec *w = scene_scan<kExact>(A, recs, o, d, t);
         hit = w != recs + A.n ? &w->s : nullptr;
     }
-    return shade<kExact>(hit, t, trig, o, d, T, E, depth, st);
+    return shade<kExact, kBvh && PTG_SHADE_PACK>(hit, t, trig, o, d, T, E, depth, st);
 }
 
-template <bool kExact>
+template <bool kExact, bool kPacked>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st)
 {
@@ -1925,7 +1932,10 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         return true;
     }
     const ShadeRec &S = *hit;
-    float4 s0 = S.s0, s1 = S.s1;
+    float4 s0 = S.s0;
+    [[maybe_unused]] float4 s1;
+    if constexpr (!kPacked)
+        s1 = S.s1;
 #if PTG_SHADE_EARLY
     // the record's reads issued first, the roulette's draw (independent of
     // them) computed while they are in flight -- held there by a scheduling
@@ -1962,7 +1972,15 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         nn = front ? on : mk3(-on.x, -on.y, -on.z);
     }
     // main.cpp:126
-    E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
+    if constexpr (kPacked) {
+        // (PTG_SHADE_PACK: s0.w bit 30 = the sphere emits; its emission read here)
+        if (__float_as_uint(s0.w) >> 30) {
+            const float4 em = S.s1;
+            E = mk3(__builtin_fmaf(T.x, em.x, E.x), __builtin_fmaf(T.y, em.y, E.y), __builtin_fmaf(T.z, em.z, E.z));
+        }
+    } else {
+        E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
+    }
     // main.cpp:128-139: Russian roulette after depth 4 (PTG_RR_ROWSEL: the
     // colour row read above by address; else both rows read and selected)
 #if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
@@ -1984,7 +2002,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     const uint32_t m_rr = draw_bits(st_rr);  // u = m_rr 2^-24; s0.w holds ceil(p 2^24) (prepare_scene)
 #endif
     st = rr ? st_rr : st;
-    const bool killed = rr & !(m_rr < __float_as_uint(s0.w));
+    const bool killed = rr & !(m_rr < (kPacked ? (__float_as_uint(s0.w) & 0x1FFFFFFu) : __float_as_uint(s0.w)));
 #else
     const float u_rr = draw(st_rr);
     st = rr ? st_rr : st;
@@ -1999,7 +2017,7 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
     // holding both materials issues them once; every lane's arithmetic is the
     // same as the per-material code (oracle sample_B).
-    const int mat = __float_as_int(s1.w);
+    const int mat = kPacked ? (int)((__float_as_uint(s0.w) >> 28) & 3u) : __float_as_int(s1.w);
     const bool isD = !killed & (mat == PTG_DIFFUSE);
     const bool isG = !killed & (mat == PTG_DIELECTRIC);
     bool spec = !killed & (mat == PTG_SPECULAR);
@@ -2736,7 +2754,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 const int sid = tr.best;
                 const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
 #endif
-                if (shade<kExact>(hrec, tr.tb, trig, o, d, T, E, depth, st))
+                if (shade<kExact, (bool)PTG_SHADE_PACK>(hrec, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
             PTG_PHASE(3);
@@ -3647,8 +3665,23 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     }
     if (linear)
         PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_lin, lin.data(), bytes, hipMemcpyHostToDevice));
-    else if (n_spheres)
-        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade, shade.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
+    else if (n_spheres) {
+        std::vector<ShadeRec> up(shade.begin(), shade.begin() + n_spheres);
+#if PTG_SHADE_PACK
+        // s0.w = ceil(p 2^24) (<= 2^24) | material << 28 | emits << 30 (the
+        // kernel's packed reader, shade<kExact, true>)
+        static_assert(PTG_RR_INT, "the packed shading record holds the integer roulette threshold");
+        for (ShadeRec &r : up) {
+            uint32_t w, m;
+            std::memcpy(&w, &r.s0.w, 4);
+            std::memcpy(&m, &r.s1.w, 4);
+            const bool emits = r.s1.x != 0.0f || r.s1.y != 0.0f || r.s1.z != 0.0f;
+            w |= (m & 3u) << 28 | (emits ? 1u << 30 : 0u);
+            std::memcpy(&r.s0.w, &w, 4);
+        }
+#endif
+        PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade, up.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
+    }
     {
         float tab[2 * kTrigEntries];
         trig_table(tab);
