@@ -311,8 +311,9 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_FAST_NO_DISC
 // fast mode: no disc < 0 compare in the candidate test -- v_sqrt_f32 of a
 // negative is NaN, so qq and den are NaN and the cross-multiplied compare
-// fails (exact: the same decisions; the exact mode's Goldschmidt sqrt is
-// finite there and keeps the compare; A/B r05zs)
+// fails (the same decisions, except that a negative denormal disc, if the
+// sqrt flushes it, reads as a tangent hit; the exact mode's Goldschmidt sqrt
+// is finite there and keeps the compare; A/B r05zs)
 #define PTG_FAST_NO_DISC 1
 #endif
 #ifndef PTG_FAST_NN
