@@ -329,6 +329,12 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_SMALL_PF2
+// (with PTG_SMALL_PREFETCH and PTG_SMALL_G0W) the first two small spheres'
+// geometry read at the scan's start, the third one test ahead (exact; box
+// -0.2 %, box_mirror -0.2 %, A/B r05zzm)
+#define PTG_SMALL_PF2 1
+#endif
 #ifndef PTG_SHADE_PACK
 // BVH scenes: the shading record's material and an emission flag packed into
 // s0.w beside the roulette threshold (bits 28-29, 30), s1 (the emission) read
@@ -817,6 +823,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     // the first small sphere's geometry (the records after the huge ones;
     // always in bounds: the sentinel follows the last record)
     const float4 pf_g0 = recs[A.end_big].g.g0, pf_g1 = recs[A.end_big].g.g1;
+#if PTG_SMALL_PF2 && PTG_SMALL_G0W
+    const float4 pf2_g0 = recs[A.end_big + 1].g.g0;  // (in bounds: the sentinel and the wall table follow)
+#endif
 #endif
     // the small spheres [i, n) (i = n after)
     auto small_spheres = [&](int &i) {
@@ -834,7 +843,14 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // each record's geometry read one test ahead (its LDS latency
             // behind the previous test; the first at the scan's start)
             const float4 a1 = r0[1].g.g0, b1 = r0[1].g.g1;
-#if PTG_BEST_IDX
+#if PTG_BEST_IDX && PTG_SMALL_PF2 && PTG_SMALL_G0W
+            (void)a1;
+            (void)b1;
+            test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
+            const float4 a2 = r0[2].g.g0;
+            test_geo(-2, pf2_g0, pf_g1, std::integral_constant<int, kSmall>{});
+            test_geo(-1, a2, pf_g1, std::integral_constant<int, kSmall>{});
+#elif PTG_BEST_IDX
             // (i = A.n - 3 here: the relative indices are constants)
             test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
             const float4 a2 = r0[2].g.g0, b2 = r0[2].g.g1;
