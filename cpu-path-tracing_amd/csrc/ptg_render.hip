@@ -330,10 +330,11 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #define PTG_RR_ROWSEL 1
 #endif
 #ifndef PTG_SMALL_PF2
-// (with PTG_SMALL_PREFETCH and PTG_SMALL_G0W) the first two small spheres'
-// geometry read at the scan's start, the third one test ahead (exact; box
-// -0.2 %, box_mirror -0.2 %, A/B r05zzm)
-#define PTG_SMALL_PF2 1
+// (with PTG_SMALL_PREFETCH and PTG_SMALL_G0W) the small spheres' geometry
+// read at the scan's start: 1 = the first two (the third one test ahead;
+// box -0.2 %, box_mirror -0.2 %, A/B r05zzm), 2 = all three (another -0.3 %
+// on both, A/B r05zzn; 58 VGPRs); exact
+#define PTG_SMALL_PF2 2
 #endif
 #ifndef PTG_SHADE_PACK
 // BVH scenes: the shading record's material and an emission flag packed into
@@ -825,6 +826,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     const float4 pf_g0 = recs[A.end_big].g.g0, pf_g1 = recs[A.end_big].g.g1;
 #if PTG_SMALL_PF2 && PTG_SMALL_G0W
     const float4 pf2_g0 = recs[A.end_big + 1].g.g0;  // (in bounds: the sentinel and the wall table follow)
+#if PTG_SMALL_PF2 >= 2
+    const float4 pf3_g0 = recs[A.end_big + 2].g.g0;  // (PTG_SMALL_PF2 = 2: all three at the start)
+#endif
 #endif
 #endif
     // the small spheres [i, n) (i = n after)
@@ -847,7 +851,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             (void)a1;
             (void)b1;
             test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
+#if PTG_SMALL_PF2 >= 2
+            const float4 a2 = pf3_g0;
+#else
             const float4 a2 = r0[2].g.g0;
+#endif
             test_geo(-2, pf2_g0, pf_g1, std::integral_constant<int, kSmall>{});
             test_geo(-1, a2, pf_g1, std::integral_constant<int, kSmall>{});
 #elif PTG_BEST_IDX
