@@ -329,6 +329,13 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 // rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
 #define PTG_RR_ROWSEL 1
 #endif
+#ifndef PTG_PRE_EARLY
+// linear kernel: the lane's prefetched camera ray read from LDS at the top of
+// each iteration (before the scan), so a path that ends in this segment
+// starts the next one without waiting on the read (A/B r05zzp: +1.7 %, the
+// 8 registers held through the segment: 64 VGPRs)
+#define PTG_PRE_EARLY 0
+#endif
 #ifndef PTG_SMALL_PF2
 // (with PTG_SMALL_PREFETCH and PTG_SMALL_G0W) the small spheres' geometry
 // read at the scan's start: 1 = the first two (the third one test ahead;
@@ -2518,11 +2525,19 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         parked = false;
     };
     // path end: park the radiance and start the prefetched ray, or wait
+    [[maybe_unused]] float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pq1 = pq0;  // PTG_PRE_EARLY
     auto path_done = [&]() {
         item = -1;
         if (has_pre) {
             const float4 *rec = pre_rec();
-            const float4 p0 = rec[0], p1 = rec[1];
+            float4 p0, p1;
+            if (PTG_PRE_EARLY && !kBvh) {
+                p0 = pq0;
+                p1 = pq1;
+            } else {
+                p0 = rec[0];
+                p1 = rec[1];
+            }
             park();
             begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
             has_pre = false;
@@ -2625,6 +2640,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
+                if constexpr (PTG_PRE_EARLY && !kBvh) {
+                    const float4 *rec = pre_rec();
+                    pq0 = rec[0];
+                    pq1 = rec[1];
+                }
                 if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
                     path_done();
             }
