@@ -342,8 +342,9 @@ def check_group(n, ranks, devices, bus_ids, rehearsal):
     known = [r for r in ranks if r is not None]
     if any(r != n for r in known):
         bad.append(f"RCCL communicators of {sorted(set(known))} ranks, not {n}")
-    if len(set(devices)) != n:
-        bad.append(f"{len(set(devices))} distinct devices for {n} ranks: {devices}")
+    kd = [d for d in devices if d is not None and d != ""]
+    if len(kd) == n and len(set(kd)) != n:
+        bad.append(f"{len(set(kd))} distinct devices for {n} ranks: {devices}")
     kb = [b for b in bus_ids if b]
     if len(kb) == n and len(set(kb)) != n:
         bad.append(f"{len(set(kb))} distinct PCI bus ids for {n} ranks: {bus_ids}")
@@ -377,11 +378,14 @@ def torch_rccl_info(local):
 
 
 def bus_id_of(device):
-    """PCI bus id of a visible device (hipDeviceGetPCIBusId via the C ABI)."""
+    """PCI bus id of a visible device (hipDeviceGetPCIBusId via the C ABI);
+    None when it cannot be read -- not evidence either way in check_group
+    (a shared 'unknown' string would read as one bus id for every rank)."""
     try:
-        return ptgpu.pci_bus_id(device)
+        return ptgpu.pci_bus_id(device) or None
     except Exception as e:  # noqa: BLE001
-        return f"unknown ({e})"
+        log(f"warning: PCI bus id of device {device} not readable: {e}")
+        return None
 
 
 def arith_flags(args):
@@ -603,14 +607,14 @@ def main(argv=None):
             else torch_rccl_info(local)
         bus = bus_id_of(local)
         rec = [cnt if cnt is not None else -1, cdev if cdev is not None else -1, urank if urank is not None else -1,
-               local] + list(bus.encode()[:32].ljust(32, b"\0"))
+               local] + list((bus or "").encode()[:32].ljust(32, b"\0"))
         gdev = torch.device("cpu") if rehearsal else dev
         mine = torch.tensor(rec, dtype=torch.int64, device=gdev)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         recs = [t.cpu().tolist() for t in allr]
         ranks = [r[0] if r[0] >= 0 else None for r in recs]
-        buses = [bytes(b for b in r[4:] if b).decode(errors="replace") for r in recs]
+        buses = [bytes(b for b in r[4:] if b).decode(errors="replace") or None for r in recs]
         # distinct devices: one process per GPU, so the bus ids name them
         bad = check_group(world, ranks, buses, buses, rehearsal)
         group = {"rccl_ranks": None if rehearsal else ranks,

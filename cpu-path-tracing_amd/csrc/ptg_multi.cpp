@@ -20,7 +20,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ptgpu.h"
@@ -43,6 +45,7 @@ struct Shard {
     size_t slab_cap = 0;  // floats
     unsigned long long *counters = nullptr;  // PTG_FLAG_COUNT_TESTS: 4 per shard
     ncclComm_t comm = nullptr;
+    bool stuck = false;  // destroy(): a broken group's stream did not drain
 };
 
 // Restores the calling thread's current HIP device on every return path.
@@ -106,19 +109,42 @@ int destroy(ptg_multi *m)
     // group's too: its communicators were aborted when the group failed, so
     // nothing queued can block, and a failed frame's render kernels may still
     // be running on the slabs
+    // A broken group's streams are drained with a bounded wait (ncclCommAbort
+    // should release every queued gather, but a peer that never returns must
+    // not hang close(): after ~10 s the buffers of that shard are leaked, not
+    // freed under a running kernel, and the call reports PTG_ERR_HIP).
+    int rc = PTG_OK;
     for (Shard &s : m->shards) {
         if (s.id < 0)
             continue;
         (void)hipSetDevice(s.id);
-        if (s.stream)
+        if (!s.stream)
+            continue;
+        if (!m->broken) {
             (void)hipStreamSynchronize(s.stream);
+            continue;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipStreamQuery(s.stream) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                s.stuck = true;
+                rc = PTG_ERR_HIP;
+                break;
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
     }
+    bool any_stuck = false;
     for (Shard &s : m->shards) {
         if (s.id < 0)
             continue;
         (void)hipSetDevice(s.id);
         if (s.comm)
             (void)(m->broken ? ncclCommAbort(s.comm) : ncclCommDestroy(s.comm));
+        if (s.stuck) {  // still running after the abort: leak its buffers
+            any_stuck = true;
+            continue;
+        }
         if (s.slab)
             (void)hipFree(s.slab);
         if (s.counters)
@@ -134,7 +160,7 @@ int destroy(ptg_multi *m)
         if (s.ctx)
             (void)ptg_context_destroy(s.ctx);
     }
-    if (!m->shards.empty() && m->shards[0].id >= 0) {
+    if (!any_stuck && !m->shards.empty() && m->shards[0].id >= 0) {
         (void)hipSetDevice(m->shards[0].id);
         if (m->gathered)
             (void)hipFree(m->gathered);
@@ -144,7 +170,7 @@ int destroy(ptg_multi *m)
             (void)hipEventDestroy(m->t_unsharded);
     }
     delete m;
-    return PTG_OK;
+    return rc == PTG_OK ? PTG_OK : fail(rc, "multi: a broken group's stream did not drain within 10 s; its buffers were leaked");
 }
 
 int create(const ptg_sphere *spheres, size_t n_spheres, const ptg_camera *cam, const int *devices, int n, bool rccl,
@@ -477,12 +503,14 @@ int ptg_multi_frame_device(ptg_multi *m, const ptg_params *params, unsigned long
     if (rc)
         return rc;
     DeviceGuard g;
+    // before reserve(): a failed re-allocation must not leave the previous
+    // frame's flag on a freed image
+    m->timed = false;
     size_t slab_elems = 0;
     if ((rc = reserve(m, params, slab_elems)))
         return rc;
     const int n = (int)m->shards.size();
     const bool count = (params->flags & (PTG_FLAG_COUNT_TESTS | PTG_FLAG_COUNT_NONFINITE)) != 0;
-    m->timed = false;
     for (int k = 0; k < n; ++k) {
         Shard &s = m->shards[k];
         MULTI_HIP(hipSetDevice(s.id));

@@ -63,9 +63,6 @@ int fail(int code, const std::string &msg)
 #ifndef PTG_BLOCK
 #define PTG_BLOCK 256  // linear-scene render kernel workgroup size
 #endif
-#ifndef PTG_TRIG_LDS
-#define PTG_TRIG_LDS 1  // linear-scene render kernel: sin/cos table in LDS (0: read through L1)
-#endif
 constexpr int kBlock = PTG_BLOCK;
 constexpr int kMaxLevels = 4;     // unit levels: head + up to 3 split-tail levels
 // samples per sub-pixel in one work unit, at most: a unit's paths are indexed
@@ -98,14 +95,8 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #ifndef PTG_LEAF_SPLIT
 #define PTG_LEAF_SPLIT 2  // BVH leaf phase: lanes without a leaf test part of another lane's leaf (1: one helper per leaf, 2: up to two)
 #endif
-#ifndef PTG_LEAF_CHUNK
-#define PTG_LEAF_CHUNK 0  // BVH: spheres of a parked leaf tested per leaf phase (0: all)
-#endif
 #ifndef PTG_LONG_LEAF
 #define PTG_LONG_LEAF 5  // BVH leaf phase: leaves of at least this many spheres get helpers first (and a second one; 5 beats 4 by 0.9 %, 3 and 6 worse)
-#endif
-#ifndef PTG_LEAF_DONE_SEL
-#define PTG_LEAF_DONE_SEL 1  // BVH (wide): leaf completion by selects for the whole wave, not divergent branches
 #endif
 #ifndef PTG_BVH_UNIT_MULT
 #define PTG_BVH_UNIT_MULT 2  // BVH scenes below the split-tail threshold: this many times more work units (8-way C5 shards: 2 beats 1 and 4 by 2-5 %)
@@ -141,15 +132,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // faster than with their samples split into ~96k units)
 #define PTG_TAIL_MIN_HALF_ROUNDS 3
 #endif
-#ifndef PTG_COOP_TAIL
-#define PTG_COOP_TAIL 1  // split-tail level with one chunk per wave of a workgroup: reduced in LDS (no HBM atomics)
-#endif
-#ifndef PTG_BVH_OCTANTS
-#define PTG_BVH_OCTANTS 1  // BVH: one depth-first layout per ray-direction octant (near child first)
-#endif
-#ifndef PTG_BVH_WIDE
-#define PTG_BVH_WIDE 1  // BVH: 4-wide nodes walked with a per-lane short stack (0: binary stackless skip walk)
-#endif
 #ifndef PTG_BVH_STACK
 #define PTG_BVH_STACK 3  // wide walk: per-lane stack entries before the continuation fallback (3: C5 -0.7 % vs 2, A/B 258.3 vs 260.1 ms)
 #endif
@@ -164,32 +146,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 #endif
 #ifndef PTG_BVH_TAIL_CHUNK
 #define PTG_BVH_TAIL_CHUNK 0  // ... in chunks of this many samples (0: the auto chunk, 20 at C5 8-way; 10: +0.8 %, 32: +5 %)
-#endif
-#ifndef PTG_BVH_TAIL_PSPLIT
-#define PTG_BVH_TAIL_PSPLIT 1  // BVH kernel's split tail: units of interleaved pixels with all samples (0: sample chunks accumulated in HBM)
-#endif
-#ifndef PTG_DG_SKIP
-#define PTG_DG_SKIP 1  // shade: skip the diffuse/dielectric block when no lane of the wave needs it
-#endif
-#ifndef PTG_DG_SPLIT
-// shade: a wave with no dielectric lane runs the diffuse sampler alone
-// (measured slower: box +0.4 %, A/B r05c)
-#define PTG_DG_SPLIT 0
-#endif
-#ifndef PTG_SMALL_DISC_SKIP
-#define PTG_SMALL_DISC_SKIP 1  // linear scan: skip a small sphere's root when no lane's disc >= 0 (box -0.9 %, box_mirror -2.1 %, simple -7 %; also skipping spheres behind every lane: +0.1-0.5 %)
-#endif
-#ifndef PTG_BOX_MODE
-#define PTG_BOX_MODE 1  // linear scenes: nearest-plane wall first (box mode, scene_scan)
-#endif
-#ifndef PTG_NODE_CASCADE
-#define PTG_NODE_CASCADE 1  // BVH node step: the first hits' words and slots by a select cascade on the box tests
-#endif
-#ifndef PTG_NODE_OFS32
-#define PTG_NODE_OFS32 1  // BVH node loads: 32-bit offsets on the SGPR base
-#endif
-#ifndef PTG_BVH_LDS_ROOT
-#define PTG_BVH_LDS_ROOT 0  // A/B: the root wide node of every octant layout read from LDS
 #endif
 #ifndef PTG_READY_FRAC
 #define PTG_READY_FRAC 6  // BVH: stop walking and shade once 6/8 of the active lanes have finished their scan
@@ -239,152 +195,6 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #ifndef PTG_WAVE_STATS
 #define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
 #endif
-#ifndef PTG_SMALL_SGPR
-#define PTG_SMALL_SGPR 0  // the three small spheres' geometry from kernel arguments (SGPRs), not LDS (A/B r05p: box +0.4 %, box_mirror -0.2 %; not kept)
-#endif
-#ifndef PTG_WALL_GEO
-// box mode: the walls' geometry copied into a table indexed by (axis, side)
-// after the offset table, the record's byte offset in g1.x and NaN geometry
-// for a missing wall (no win) -- one LDS round trip per scan instead of two
-// (with PTG_DEPTH_EARLY: box -1.0 %, box_mirror -1.0 %, A/B r05q)
-#define PTG_WALL_GEO 1
-#endif
-#ifndef PTG_DEPTH_EARLY
-#define PTG_DEPTH_EARLY 1  // shade: depth counted before the sky branch (no per-branch copy; A/B r05q)
-#endif
-#ifndef PTG_WALLS_LAST
-#define PTG_WALLS_LAST 0  // fast box mode: the small spheres tested before the extra walls (A/B)
-#endif
-#ifndef PTG_SMALL_FIRST
-// fast box mode: the small spheres tested between the nearest wall's LDS read
-// and its test (the read's latency behind their work; only exact ties
-// between a wall and a small sphere can resolve differently; A/B)
-#define PTG_SMALL_FIRST 0
-#endif
-#ifndef PTG_SMALL_PREFETCH
-#define PTG_SMALL_PREFETCH 1  // the three small spheres' records read one test ahead, the first at the scan's start (box -0.2 %, box_mirror -0.3 %, A/B r05t)
-#endif
-#ifndef PTG_INROOM_EARLY
-#define PTG_INROOM_EARLY 0  // box mode: the room-bound compares before the wall test (A/B)
-#endif
-#ifndef PTG_SHADE_EARLY
-#define PTG_SHADE_EARLY 0  // shade: the hit record's reads first, the roulette's draw in their shadow (A/B; needs PTG_RR_INT)
-#endif
-#ifndef PTG_LIN_UNROLL2
-#define PTG_LIN_UNROLL2 0  // linear kernel: the main loop's body twice (A/B)
-#endif
-#ifndef PTG_D_INPLACE
-#define PTG_D_INPLACE 0  // shade: the next direction written into d in place (A/B)
-#endif
-#ifndef PTG_FAST_C_FOLD
-#define PTG_FAST_C_FOLD 1  // fast mode, small spheres: c = |e|^2 - R^2 with -R^2 folded into the first fma (box -0.8 %, box_mirror -0.9 %, quality rows unchanged; A/B r05zd)
-#endif
-#ifndef PTG_FAST_C_FOLD_BVH
-#define PTG_FAST_C_FOLD_BVH 0  // the same for the BVH leaf spheres (A/B)
-#endif
-#ifndef PTG_DRAW_MERGE
-#define PTG_DRAW_MERGE 1  // shade: every lane's first BRDF draw taken once before the samplers (exact; box -1.4 %, A/B r05zi)
-#endif
-#ifndef PTG_DRAW2_MERGE
-#define PTG_DRAW2_MERGE 0  // shade (with PTG_DRAW_MERGE): every lane's second BRDF draw taken once too (A/B)
-#endif
-#ifndef PTG_U1_HOIST
-#define PTG_U1_HOIST 1  // shade (with PTG_DRAW_MERGE): the first draw's value converted once (exact; A/B r05zl)
-#endif
-#ifndef PTG_CTH_MIN
-#define PTG_CTH_MIN 1  // shade, fast mode: cos theta clamped by v_min_f32 (with PTG_U1_HOIST box -0.45 %, box_mirror -0.25 %; A/B r05zl)
-#endif
-#ifndef PTG_FRES_IN_BLOCK
-#define PTG_FRES_IN_BLOCK 1  // shade: a Fresnel reflection's second draw taken in the Fresnel block, not the mirror block (exact; box_mirror -0.9 %, box +-0; A/B r05zm)
-#endif
-#ifndef PTG_XWALL_GEO
-#define PTG_XWALL_GEO 1  // box mode's extra walls from the wall geometry table (one LDS read per pass instead of two; exact; box_mirror -0.6 %, A/B r05zn)
-#endif
-#ifndef PTG_BEST_IDX
-// linear scan: the winner kept as a record index relative to the sentinel
-// (the three small spheres -3, -2, -1: inline constants, no v_mov per
-// select; the wall table holds the walls' relative indices), the record
-// address formed once after the scan (exact: bookkeeping only; with
-// PTG_FAST_NO_DISC box -0.2 %, box_mirror -0.5 %, A/B r05zs)
-#define PTG_BEST_IDX 1
-#endif
-#ifndef PTG_FAST_NO_DISC
-// fast mode: no disc < 0 compare in the candidate test -- v_sqrt_f32 of a
-// negative is NaN, so qq and den are NaN and the cross-multiplied compare
-// fails (the same decisions, except that a negative denormal disc, if the
-// sqrt flushes it, reads as a tangent hit; the exact mode's Goldschmidt sqrt
-// is finite there and keeps the compare; A/B r05zs)
-#define PTG_FAST_NO_DISC 1
-#endif
-#ifndef PTG_FAST_NN
-// shade, fast mode: the facing normal as (p - C) (+-1/R) with the side from
-// (p - C).d (one select instead of three), the mirror's n.d from that dot
-// (one mul instead of a dot product); another rounding of the same values
-// (box -0.2 %, box_mirror -0.2 %, A/B r05zz)
-#define PTG_FAST_NN 1
-#endif
-#ifndef PTG_RR_ROWSEL
-// shade: the roulette's colour row (s2, or s3 = s2 / p past the roulette
-// depth) selected by address -- one record read, no selects; 1/R is in both
-// rows' w (exact; box -0.4 %, box_mirror -0.4 %, C5 +-0; A/B r05zzc)
-#define PTG_RR_ROWSEL 1
-#endif
-#ifndef PTG_PRE_EARLY
-// linear kernel: the lane's prefetched camera ray read from LDS at the top of
-// each iteration (before the scan), so a path that ends in this segment
-// starts the next one without waiting on the read (A/B r05zzp: +1.7 %, the
-// 8 registers held through the segment: 64 VGPRs)
-#define PTG_PRE_EARLY 0
-#endif
-#ifndef PTG_SMALL_PF2
-// (with PTG_SMALL_PREFETCH and PTG_SMALL_G0W) the small spheres' geometry
-// read at the scan's start: 1 = the first two (the third one test ahead;
-// box -0.2 %, box_mirror -0.2 %, A/B r05zzm), 2 = all three (another -0.3 %
-// on both, A/B r05zzn; 58 VGPRs); exact
-#define PTG_SMALL_PF2 2
-#endif
-#ifndef PTG_SHADE_PACK
-// BVH scenes: the shading record's material and an emission flag packed into
-// s0.w beside the roulette threshold (bits 28-29, 30), s1 (the emission) read
-// only by lanes that hit an emitter -- two 16-B global loads per hit instead
-// of three (exact: the same values; A/B r05zzl: C5 +-0)
-#define PTG_SHADE_PACK 0
-#endif
-#ifndef PTG_BIG_SCALAR
-// BVH scan: the huge spheres' records (wave-uniform addresses) read through
-// the constant address space -- scalar loads, not 64-lane vector loads whose
-// data the texture data path (TD, 94 % busy on C5) returns to every lane
-// (C5 -0.3 %, A/B r05zzj)
-#define PTG_BIG_SCALAR 1
-#endif
-#ifndef PTG_SMALL_G0W
-// linear scan: a small sphere's -R^2 also in g0.w (prepare_scene), so its
-// test reads one 16-B word of its record (ds_read_b128) instead of g0.xyz
-// and g1.w (exact; box -0.3 %, box_mirror -0.2 %, A/B r05zzg)
-#define PTG_SMALL_G0W 1
-#endif
-#ifndef PTG_LEAF_NOBRANCH
-// BVH leaf loop: every candidate's scene index loaded and the lex update as
-// selects, no branch on t <= tb (A/B r05zzf: C5 +2.6 %)
-#define PTG_LEAF_NOBRANCH 0
-#endif
-#ifndef PTG_SHADE_LEAF
-// (with PTG_BEST_LEAF) the shading records also in leaf order (the huge
-// spheres before them), addressed by the winner's code directly: no scene
-// index is read to shade (A/B r05zze: C5 +4.5 % with PTG_BEST_LEAF, which
-// alone costs +5.9 % there -- the codes' tie branch in the leaf loop, not
-// the index load, is the cost)
-#define PTG_SHADE_LEAF 0
-#endif
-#ifndef PTG_BEST_LEAF
-// BVH scan: the winner kept as its leaf-order index (huge sphere k: -2 - k)
-// and turned into its scene index once, when the scan ends -- no dependent
-// scene-index load per winning candidate in the leaf loop; an exact tie of t
-// reads both scene indices (the lex rule, the same winner; A/B r05zza: C5
-// +5.3 % -- the one load at the scan's end sits right before shading, while
-// the leaf loop's loads were hidden)
-#define PTG_BEST_LEAF 0
-#endif
 #ifndef PTG_MIN_WAVES_PER_EU
 #define PTG_MIN_WAVES_PER_EU 8  // 8 waves per SIMD: <= 64 VGPRs and <= 80 SGPRs (8 blocks of 256 per CU)
 #endif
@@ -413,7 +223,6 @@ inline bool is_huge(const ptg_sphere &sp, const ptg_camera *cam)
 struct KArgs {
     const LinRec *lin;      // linear scenes (<= kLinearMax): n records in scan order + sentinel
     const ShadeRec *shade;  // BVH scenes: shading records in scene index order
-    const ShadeRec *shade_leaf;  // PTG_SHADE_LEAF: the same by winner code (leaf j at [j], huge sphere k at [-2 - k])
     int n;
     // linear scenes: records in SCAN order (prepare_scan_order), grouped by
     // kind: [0, end_ax[0]) huge spheres anchored on the x axis, then y, then z
@@ -434,12 +243,6 @@ struct KArgs {
     // tangent planes (+-inf: none); pair_lo/hi bound the room on every
     // axis (+-kFarPlane where open)
     int box_mode;
-    // PTG_SMALL_SGPR: the three small spheres' geometry {C, -R^2} when the
-    // scan ends with exactly three (the box scenes), read as kernel
-    // arguments (scalar registers), not from LDS
-#if PTG_SMALL_SGPR
-    float small_geo[3][4];
-#endif
     int rec_plus[3], rec_minus[3];  // byte offsets of the records
     float plane_plus[3], plane_minus[3];
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
@@ -451,12 +254,12 @@ struct KArgs {
     const GeoRec *big_geo;    // huge spheres, tested linearly
     const int *big_id;
     int n_nodes, n_big;
-    // PTG_BVH_OCTANTS: 8 depth-first layouts of the tree (bvh_build.hpp
+    // 8 depth-first layouts of the tree (bvh_build.hpp
     // order_bvh), layout k at node index k << bvh_shift, skip words absolute;
     // a walk is done when (ni & bvh_mask) reaches n_nodes
     int bvh_shift, bvh_mask;
     int bvh_oct_mask;  // direction-sign bits that select the layout (x 1, y 2, z 4): bvh_octant_mask
-    const int *bvh_cont;  // PTG_BVH_WIDE: per wide node (first record / 4) its continuation (bvh_build.hpp wide_conts)
+    const int *bvh_cont;  // per wide node (first record / 4) its continuation (bvh_build.hpp wide_conts)
     const float2 *trig;  // {cos, sin}(2 pi k / 128), staged in LDS (sincos2pi_tab)
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
     float pos_x, pos_y, pos_z;
@@ -537,15 +340,8 @@ __device__ __forceinline__ void camera_ray(const CamC &C, const Lane &L, uint32_
     // camera.cpp:19-30: rejection sample of the unit disk (2 draws per try)
     float px, py;
     do {
-#if PTG_RR_INT
-        // 2 u - 1 with u = m 2^-24: 2^-23 m - 1, the same exact product
-        // (the draw's scale folded into the fma)
-        px = __builtin_fmaf(0x1p-23f, (float)draw_bits(st), -1.0f);
-        py = __builtin_fmaf(0x1p-23f, (float)draw_bits(st), -1.0f);
-#else
         px = __builtin_fmaf(2.0f, draw(st), -1.0f);
         py = __builtin_fmaf(2.0f, draw(st), -1.0f);
-#endif
     } while (__builtin_fmaf(py, py, px * px) >= 1.0f);
     // camera.cpp:34-37 (offset = rd*s + rd*t, the reference's lens quirk)
     float sst = fs + ft;
@@ -582,71 +378,9 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 #ifndef PTG_UNIT_ROUNDS
 #define PTG_UNIT_ROUNDS 2  // linear scenes below the split-tail size: work units for this many rounds of wave slots (2 beats 4 by 5 %, 12 by 12 % on C1)
 #endif
-#ifndef PTG_WALL_OUT
-#define PTG_WALL_OUT 1  // fast mode, box mode: the nearest wall's outside-only root (KArgs::box_walls_out)
-#endif
-#ifndef PTG_BVH_LAYOUT_PAD
-// wide BVH: records of padding between the octant layouts (a multiple of 4;
-// 0: layouts exactly 2^k records apart, so the 8 copies of a node alias in
-// the caches' set index)
-#define PTG_BVH_LAYOUT_PAD 0
-#endif
-#ifndef PTG_BVH_Q8
-// wide BVH: 48-B nodes (8-bit planes on a per-node grid, bvh_build.hpp
-// wide_q8): three 16-B loads per node step instead of four (A/B)
-#define PTG_BVH_Q8 0
-#endif
-#ifndef PTG_BVH_Q8_STRIDE
-#define PTG_BVH_Q8_STRIDE 48  // bytes per 48-B node in the array (64: 16-B padded, line-aligned; A/B)
-#endif
-#ifndef PTG_BVH_INTERLEAVE
-// wide BVH: the 8 octant layouts interleaved node by node -- node j of
-// layout k at 8 j + k, the copies of a node in one 512-B block.  Laid out
-// 2^k records apart they aliased in the L1's set index: C5 225.9-226.2 ->
-// 218.3-218.5 ms (A/B r05c; a 4-record pad between the layouts gets 219.1-219.3)
-#define PTG_BVH_INTERLEAVE 1
-#endif
-#ifndef PTG_SMALL_UNROLL
-// linear scan: three small spheres (the box scenes) as straight-line code on
-// one LDS base address (box -0.6 %, box_mirror -0.7 %, A/B r05b/r05c)
-#define PTG_SMALL_UNROLL 1
-#endif
-#ifndef PTG_RR_INT
-// Russian roulette as an integer compare of the draw's 24 bits, the disk
-// draws' 2^-24 folded into their fma (exact: the same decisions and values;
-// box -0.5 %, box_mirror -0.6 %, A/B r05j)
-#define PTG_RR_INT 1
-#endif
-#ifndef PTG_DG_NOINIT
-// shade: the diffuse sampler's values not zero-initialised for the other
-// lanes (3 v_mov fewer per segment in waves with diffuse lanes: box -0.6 %,
-// box_mirror -0.4 %, A/B r05k)
-#define PTG_DG_NOINIT 1
-#endif
 
-#ifndef PTG_KN_MASKS
-// box mode: the nearest plane's axis kept as lane masks and its wall-table
-// byte offset selected directly (the axis index had been re-compared and
-// re-multiplied); with PTG_NEED_NOINF box -2.1 %, box_mirror -2.1 % (A/B r05p)
-#define PTG_KN_MASKS 1
-#endif
 
-#ifndef PTG_NEED_NOINF
-#define PTG_NEED_NOINF 1  // box mode (with PTG_KN_MASKS): need[] without the u < inf guard (exact, see need[])
-#endif
 
-#ifndef PTG_NODE_POP_SEL
-#define PTG_NODE_POP_SEL 0  // BVH node step: the stack pop as selects, not a divergent branch (A/B)
-#endif
-#ifndef PTG_SMALL_AC
-#define PTG_SMALL_AC 0  // fast mode, small spheres: the near root as (hb^2 - disc) / (a qq) (A/B)
-#endif
-#ifndef PTG_LEAF_NT
-#define PTG_LEAF_NT 0  // BVH leaf sphere records loaded non-temporal (A/B)
-#endif
-#ifndef PTG_BOX_WALL_LOOP
-#define PTG_BOX_WALL_LOOP 1  // box mode: extra walls one per lane per pass, with the exact cull (0: per-axis branches)
-#endif
 
 __device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
@@ -658,13 +392,9 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     // compared by cross-multiplication, only the winner is divided
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
-#if PTG_BEST_IDX
     int bi = 0;  // the winner: recs + A.n + bi (0: the sentinel, no hit)
     auto ri_of = [&](const LinRec *r) { return (int)(r - recs) - A.n; };
-#else
-    const LinRec *best = recs + A.n;
-#endif
-    // r: the record (PTG_BEST_IDX: its index relative to the sentinel)
+    // r: the record's index relative to the sentinel
     auto test_geo = [&](const auto r, const float4 g0, const float4 g1, auto kind_tag, const float un = 0.0f,
                         const float vn = 0.0f, const bool valid = true, const int ks = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
@@ -711,14 +441,12 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
         } else {
             hb = ed;
-#if PTG_FAST_C_FOLD
             // fast mode: -R^2 folded into the first product of e.e (one add
             // fewer; another rounding order of the same sum)
             if constexpr (!kExact)
-                c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, PTG_SMALL_G0W ? g0.w : g1.w)));
+                c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, g0.w)));
             else
-#endif
-            c = ee + (PTG_SMALL_G0W ? g0.w : g1.w);  // g1.w = -R^2 (PTG_SMALL_G0W: g0.w too)
+            c = ee + g0.w;  // g0.w = g1.w = -R^2
         }
         float disc;
         if constexpr (kKind == kSmall) {
@@ -730,11 +458,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // 5e-5).  Huge spheres keep hb^2 - a c: there the anchored hb, c
             // are accurate and a R^2 would be ~1e12.
             const f3 x = cross3(e, d);
-            disc = __builtin_fmaf(a, -(PTG_SMALL_G0W ? g0.w : g1.w), -dot3(x, x));
+            disc = __builtin_fmaf(a, -g0.w, -dot3(x, x));
         } else {
             disc = __builtin_fmaf(hb, hb, -(a * c));
         }
-#if PTG_SMALL_DISC_SKIP
         // a small sphere no lane's ray line meets cannot win: the wave skips
         // the root (exact: "win" below requires disc >= 0)
         if constexpr (kKind == kSmall) {
@@ -743,7 +470,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 return;
             PTG_STAT(2);
         }
-#endif
         // disc < 0 is rejected below whatever sq is: no clamp
         const float sq = Math<kExact>::sqrt(disc);
         const bool neg = hb < 0.0f;
@@ -762,17 +488,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // spheres moved paths there (item 12): not done.
             num = c;
             den = qq;
-#if PTG_SMALL_AC
-        } else if constexpr (kKind == kSmall && !kExact) {
-            // fast mode: a c = hb^2 - disc (the identity the Lagrange
-            // discriminant comes from), so the near root c/qq is kept as
-            // (a c)/(a qq) -- no e.e, two VALU fewer per sphere (A/B)
-            const float ac = __builtin_fmaf(hb, hb, -disc);
-            const float aq = a * qq;
-            const bool near_lt = ac < kEps * aq;
-            num = neg ? (near_lt ? qq : ac) : -ac;
-            den = (neg & near_lt) ? a : aq;
-#endif
         } else {
             const bool near_lt = c < kEps * qq;
             num = neg ? (near_lt ? qq : c) : -c;
@@ -780,25 +495,17 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         }
         // one eps test covers all three cases (for the near root it repeats
         // near_lt, which is false there)
-        bool win = valid & ((PTG_FAST_NO_DISC && !kExact) || !(disc < 0.0f)) & !(num < kEps * den) &
+        bool win = valid & (!kExact || !(disc < 0.0f)) & !(num < kEps * den) &
                    (num * bq < bn * den);
         if constexpr (kKind == kAxAnyOut)
             win = win & neg;
         bn = win ? num : bn;
         bq = win ? den : bq;
-#if PTG_BEST_IDX
         bi = win ? r : bi;
-#else
-        best = win ? r : best;
-#endif
     };
     auto test_rec = [&](const LinRec *r, auto kind_tag, const float un = 0.0f, const float vn = 0.0f,
                         const bool valid = true, const int ks = 0) {
-#if PTG_BEST_IDX
         test_geo(ri_of(r), r->g.g0, r->g.g1, kind_tag, un, vn, valid, ks);
-#else
-        test_geo(r, r->g.g0, r->g.g1, kind_tag, un, vn, valid, ks);
-#endif
     };
     auto test = [&](const int i, auto kind_tag) { test_rec(recs + i, kind_tag); };
     // scan order: axis-anchored walls (x, y, z), general huge spheres, small
@@ -827,64 +534,28 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #ifndef PTG_ASSUME_BOX_MODE
 #define PTG_ASSUME_BOX_MODE 0  // analysis builds only (tools/isa_breakdown.py): box mode on, the other scan compiled out
 #endif
-#if PTG_SMALL_PREFETCH
     // the first small sphere's geometry (the records after the huge ones;
     // always in bounds: the sentinel follows the last record)
     const float4 pf_g0 = recs[A.end_big].g.g0, pf_g1 = recs[A.end_big].g.g1;
-#if PTG_SMALL_PF2 && PTG_SMALL_G0W
     const float4 pf2_g0 = recs[A.end_big + 1].g.g0;  // (in bounds: the sentinel and the wall table follow)
-#if PTG_SMALL_PF2 >= 2
-    const float4 pf3_g0 = recs[A.end_big + 2].g.g0;  // (PTG_SMALL_PF2 = 2: all three at the start)
-#endif
-#endif
-#endif
+    const float4 pf3_g0 = recs[A.end_big + 2].g.g0;  // (all three read at the start)
     // the small spheres [i, n) (i = n after)
     auto small_spheres = [&](int &i) {
-#if PTG_SMALL_UNROLL
         // three small spheres (the box scenes): straight-line code on one LDS
         // base address (the records at constant offsets), no loop control
         if (A.n - i == 3) {
             const LinRec *r0 = recs + i;
-#if PTG_SMALL_SGPR
-            // the records' geometry words as kernel arguments (the same values)
-            for (int k = 0; k < 3; ++k)
-                test_geo(r0 + k, make_float4(A.small_geo[k][0], A.small_geo[k][1], A.small_geo[k][2], 0.0f),
-                         make_float4(0.0f, 0.0f, 0.0f, A.small_geo[k][3]), std::integral_constant<int, kSmall>{});
-#elif PTG_SMALL_PREFETCH
             // each record's geometry read one test ahead (its LDS latency
             // behind the previous test; the first at the scan's start)
             const float4 a1 = r0[1].g.g0, b1 = r0[1].g.g1;
-#if PTG_BEST_IDX && PTG_SMALL_PF2 && PTG_SMALL_G0W
             (void)a1;
             (void)b1;
             test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
-#if PTG_SMALL_PF2 >= 2
             const float4 a2 = pf3_g0;
-#else
-            const float4 a2 = r0[2].g.g0;
-#endif
             test_geo(-2, pf2_g0, pf_g1, std::integral_constant<int, kSmall>{});
             test_geo(-1, a2, pf_g1, std::integral_constant<int, kSmall>{});
-#elif PTG_BEST_IDX
-            // (i = A.n - 3 here: the relative indices are constants)
-            test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
-            const float4 a2 = r0[2].g.g0, b2 = r0[2].g.g1;
-            test_geo(-2, a1, b1, std::integral_constant<int, kSmall>{});
-            test_geo(-1, a2, b2, std::integral_constant<int, kSmall>{});
-#else
-            test_geo(r0, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
-            const float4 a2 = r0[2].g.g0, b2 = r0[2].g.g1;
-            test_geo(r0 + 1, a1, b1, std::integral_constant<int, kSmall>{});
-            test_geo(r0 + 2, a2, b2, std::integral_constant<int, kSmall>{});
-#endif
-#else
-            test_rec(r0, std::integral_constant<int, kSmall>{});
-            test_rec(r0 + 1, std::integral_constant<int, kSmall>{});
-            test_rec(r0 + 2, std::integral_constant<int, kSmall>{});
-#endif
             i = A.n;
         }
-#endif
         for (; i < A.n; ++i)
             test(i, std::integral_constant<int, kSmall>{});
     };
@@ -901,9 +572,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // k's + wall (2k) and - wall (2k + 1), -1 where missing
         [[maybe_unused]] const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
         float u[3], v[3];
-#if PTG_KN_MASKS
         bool posk[3];
-#endif
         for (int k = 0; k < 3; ++k) {
             // the uniform plane / record values stay in SGPRs: select values,
             // not kernel-argument addresses (that became per-lane loads)
@@ -918,11 +587,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             const float up = pp - comp(o, k), um = comp(o, k) - pm;
             u[k] = pos ? up : um;
             v[k] = __builtin_fabsf(dk);
-#if PTG_KN_MASKS
             posk[k] = pos;
-#endif
         }
-#if PTG_KN_MASKS
         // the same selection as below, kept as lane masks (is_k) and the wall
         // table's byte offset of the selected wall (8 k, + 4 for the - wall),
         // not as an axis index re-compared and re-multiplied
@@ -937,74 +603,17 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         vn = n2 ? v[2] : vn;
         offn = n2 ? (posk[2] ? 16 : 20) : offn;
         const bool isk[3] = {!(n1 | n2), (bool)(n1 & !n2), n2};
-#if !PTG_WALL_GEO
-        const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls) + offn);
-#endif
-#else
-        float un = u[0], vn = v[0];
-        int kn = 0;
-        for (int k = 1; k < 3; ++k) {
-            const bool nearer = u[k] * vn < un * v[k];
-            un = nearer ? u[k] : un;
-            vn = nearer ? v[k] : vn;
-            kn = nearer ? k : kn;
-        }
-        // kn's wall is missing only when no existing wall the ray moves
-        // toward has v > 0 (every such plane is parallel to the ray): then no
-        // wall can be hit from inside the room, and the test is masked
-        // (the byte offset selected directly: an index select became a
-        // v_cndmask 0/1 and a shift)
-        const int in = *reinterpret_cast<const int *>(reinterpret_cast<const char *>(walls + 2 * kn) +
-                                                      (comp(d, kn) >= 0.0f ? 0 : 4));
-#endif
         [[maybe_unused]] auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
-#if PTG_INROOM_EARLY
-        bool in_room;
-#endif
-#if PTG_WALL_GEO && PTG_KN_MASKS
         {
             // 32-B geometry entries, entry 2 k + side at 8 offn bytes
             const GeoRec *wg = reinterpret_cast<const GeoRec *>(recs + A.n + 2);
             const GeoRec &g = *reinterpret_cast<const GeoRec *>(reinterpret_cast<const char *>(wg) + 8 * offn);
             const float4 g0 = g.g0, g1 = g.g1;
-#if PTG_SMALL_FIRST
-            if constexpr (!kExact) {
-                int j = A.end_ax[2];
-                small_spheres(j);
-            }
-#endif
-#if PTG_INROOM_EARLY
-            // (independent of the wall test: its compares issued while the
-            // wall record's LDS read is in flight -- held there by a
-            // scheduling barrier)
-            in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
-                      (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
-            __builtin_amdgcn_sched_barrier(0);
-#endif
-#if PTG_BEST_IDX
             test_geo(__float_as_int(g1.x), g0, g1,
-#else
-            test_geo(rec_at(__float_as_int(g1.x)), g0, g1,
-#endif
-                     std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{}, un, vn);
+                     std::integral_constant<int, !kExact ? kAxAnyOut : kAxAny>{}, un, vn);
         }
-#else
-        test_rec(rec_at(in >= 0 ? in : 0), std::integral_constant<int, (PTG_WALL_OUT && !kExact) ? kAxAnyOut : kAxAny>{},
-                 un, vn, in >= 0);
-#endif
-#if PTG_WALLS_LAST
-        // fast mode: the small spheres before the extra walls (box mode has
-        // no other huge sphere: they follow the walls in the scan), so the
-        // wall test's LDS read overlaps their first instructions and need[]
-        // culls against the nearer winner; only exact ties between an extra
-        // wall and a small sphere can resolve differently
-        if constexpr (!kExact) {
-            int j = A.end_ax[2];
-            small_spheres(j);
-        }
-#endif
         const float bqm = bq * kPlaneMargin;
         bool need[3];
         for (int k = 0; k < 3; ++k) {
@@ -1012,25 +621,17 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // holds for any v (also guarded explicitly by u < inf -- a test of
             // values: selecting the kernel-argument record offsets per lane
             // compiled to three dependent global loads)
-#if PTG_KN_MASKS && PTG_NEED_NOINF
             // (no u < inf guard: a missing wall's need is false unless bn v
             // is NaN, and the pass below masks a missing wall's test by its
             // table offset -1 -- the same results)
             need[k] = !isk[k] & !(bn * v[k] < u[k] * bqm);
-#elif PTG_KN_MASKS
-            need[k] = !isk[k] & (u[k] < HUGE_VALF) & !(bn * v[k] < u[k] * bqm);
-#else
-            need[k] = (k != kn) & (u[k] < HUGE_VALF) & !(bn * v[k] < u[k] * bqm);
-#endif
         }
         // a wall the ray moves away from can be hit only from beyond its
         // tangent plane (outside the room's bound on that side -- after a
         // bounce off a curved wall far from its tangent point, frequent in
         // box_mirror's mirror tube); a missing wall's bound is +-kFarPlane
-#if !PTG_INROOM_EARLY
         const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
                              (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
-#endif
         if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
             PTG_STAT(3);
 #if PTG_BLOCK_STATS == 3  // debug: wave cycles of the extra-wall block in [15]
@@ -1048,7 +649,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 }
             }
 #endif
-#if PTG_BOX_WALL_LOOP
             // each lane's extra walls in the order of the scan below (toward
             // x, y, z, then away x, y, z): one wall per lane per pass, so a
             // wave pays one test per pass, not one per axis any lane needs
@@ -1071,54 +671,15 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                 m &= m - 1u;
                 const int k = j < 3 ? j : (j < 6 ? j - 3 : 0);
                 const bool toward = j < 3;
-#if PTG_XWALL_GEO && PTG_WALL_GEO
                 // the wall's geometry entry (axis, side) of the table above:
                 // one dependent LDS read; a missing wall's NaN geometry never
                 // passes the cull's compares' win
                 const int side = (comp(d, k) >= 0.0f) == toward ? 0 : 1;
                 const GeoRec &gx = reinterpret_cast<const GeoRec *>(recs + A.n + 2)[2 * k + side];
                 const float4 x0 = gx.g0, x1 = gx.g1;
-#if PTG_BEST_IDX
                 test_geo(__float_as_int(x1.x), x0, x1, std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
-#else
-                test_geo(rec_at(__float_as_int(x1.x)), x0, x1, std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
-#endif
                          j < 6, k);
-#else
-                const int off = walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)];
-                test_rec(rec_at(off >= 0 ? off : 0), std::integral_constant<int, kAxSel>{}, 0.0f, 0.0f,
-                         (j < 6) & (off >= 0), k);
-#endif
             }
-#else
-            auto wall = [&](int k, bool toward) {
-                return rec_at(walls[2 * k + ((comp(d, k) >= 0.0f) == toward ? 0 : 1)]);
-            };
-            if (need[0])
-                test_rec(wall(0, true), std::integral_constant<int, kAxX>{});
-            if (need[1])
-                test_rec(wall(1, true), std::integral_constant<int, kAxY>{});
-            if (need[2])
-                test_rec(wall(2, true), std::integral_constant<int, kAxZ>{});
-            if (__ballot(!in_room) != 0ull) {
-                bool away[3];
-                for (int k = 0; k < 3; ++k) {
-                    float pp = A.plane_plus[k], pm = A.plane_minus[k], lo = A.pair_lo[k], hi = A.pair_hi[k];
-                    asm volatile("" : "+s"(pp), "+s"(pm), "+s"(lo), "+s"(hi));
-                    const float ok = comp(o, k);
-                    const bool pos = comp(d, k) >= 0.0f;
-                    // (the wall's existence checked by value as well: a NaN
-                    // origin must not select a missing wall's record)
-                    away[k] = pos ? (!(ok >= lo) & (pm > -HUGE_VALF)) : (!(ok <= hi) & (pp < HUGE_VALF));
-                }
-                if (away[0])
-                    test_rec(wall(0, false), std::integral_constant<int, kAxX>{});
-                if (away[1])
-                    test_rec(wall(1, false), std::integral_constant<int, kAxY>{});
-                if (away[2])
-                    test_rec(wall(2, false), std::integral_constant<int, kAxZ>{});
-            }
-#endif
 #if PTG_BLOCK_STATS == 3
             {
                 const unsigned long long xw_t1 = clock64();
@@ -1127,7 +688,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             }
 #endif
         }
-        i = ((PTG_WALLS_LAST || PTG_SMALL_FIRST) && !kExact) ? A.n : A.end_ax[2];
+        i = A.end_ax[2];
     } else {
         axis_group(std::integral_constant<int, kAxX>{});
         axis_group(std::integral_constant<int, kAxY>{});
@@ -1136,13 +697,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     for (; i < A.end_big; ++i)
         test(i, std::integral_constant<int, kBig>{});
     small_spheres(i);
-#if PTG_BEST_IDX
     tbest = bi != 0 ? Math<kExact>::div(bn, bq) : kInf;
     return recs + A.n + bi;
-#else
-    tbest = best != recs + A.n ? Math<kExact>::div(bn, bq) : kInf;
-    return best;
-#endif
 }
 
 // Scenes with more than kLinearMax spheres: the huge
@@ -1178,13 +734,6 @@ __device__ __forceinline__ float root_lex(const float4 g0, const float4 g1, cons
         c = __builtin_fmaf(g1.w, dot3(e, mk3(g1.x, g1.y, g1.z)), ee);
     } else {
         hb = ed;
-#if PTG_FAST_C_FOLD_BVH
-        // fast mode: -R^2 folded into the first fma of e.e (as scene_scan's
-        // small spheres, PTG_FAST_C_FOLD)
-        if constexpr (!kExact)
-            c = __builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, __builtin_fmaf(e.x, e.x, g0.w)));
-        else
-#endif
         c = ee + g0.w;  // g0.w = -R^2
     }
     // the two culls and the discriminant test as one early-out (bitwise: the
@@ -1250,23 +799,6 @@ __device__ __forceinline__ void update_lex(const float t, const int sid, float &
 // SGPRs lose their address space, and generic (flat) loads also wait on LDS
 template <class T>
 using gptr = const T __attribute__((address_space(1))) *;
-#if PTG_BEST_LEAF
-// PTG_BEST_LEAF: a winner code -> its scene index (-1: none)
-__device__ __forceinline__ int sid_of(const KArgs &A, const int c)
-{
-    return c >= 0 ? ((gptr<int>)A.bvh_id)[c] : (c == -1 ? -1 : ((gptr<int>)A.big_id)[-2 - c]);
-}
-// update_lex on winner codes: a nearer t wins; an exact tie reads both scene
-// indices (rare) and the lower wins, as update_lex
-__device__ __forceinline__ void update_lex_c(const KArgs &A, const float t, const int c, float &tb, int &best)
-{
-    bool win = t < tb;
-    if (t == tb)
-        win = (unsigned)sid_of(A, c) < (unsigned)sid_of(A, best);
-    tb = win ? t : tb;
-    best = win ? c : best;
-}
-#endif
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // a compact node record, loadable from gptr
 
 struct BvhTrav {
@@ -1274,7 +806,6 @@ struct BvhTrav {
     int pend;  // parked leaf (first | count << 24) or -1
     float tb;  // nearest root so far
     int best;  // winner's scene index or -1
-#if PTG_BVH_WIDE
     // wide walk: ni = the next position (a wide node's first record + the
     // slot to resume from, >= 0), -1 (walk finished), or -- only while a leaf
     // is parked -- kPopLater (-2: pop the stack after the leaf phase) or a
@@ -1289,10 +820,8 @@ struct BvhTrav {
     int s2;
 #endif
     int res;
-#endif
 };
 
-#if PTG_BVH_WIDE
 __device__ __forceinline__ bool bvh_done(const KArgs &, const BvhTrav &tr) { return (tr.ni == -1) & (tr.pend < 0); }
 __device__ __forceinline__ int bvh_pop(gptr<int> cont, BvhTrav &tr)
 {
@@ -1311,12 +840,6 @@ __device__ __forceinline__ int bvh_pop(gptr<int> cont, BvhTrav &tr)
         tr.res = cont[r >> 2];
     return r;
 }
-#else
-__device__ __forceinline__ bool bvh_done(const KArgs &A, const BvhTrav &tr)
-{
-    return tr.pend < 0 && (tr.ni & A.bvh_mask) >= A.n_nodes;
-}
-#endif
 
 // Start a scan: the huge spheres (tested linearly, first), then the BVH in
 // the layout of the ray's direction octant.
@@ -1326,7 +849,6 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     const float a = dot3(d, d);
     tr.tb = kInf;
     tr.best = -1;
-#if PTG_BIG_SCALAR
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     typedef const __attribute__((address_space(4))) f32x4 *cvec_t;
     typedef const __attribute__((address_space(4))) int *cint_t;
@@ -1337,33 +859,13 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
         const float4 g0 = make_float4(v0.x, v0.y, v0.z, v0.w), g1 = make_float4(v1.x, v1.y, v1.z, v1.w);
         update_lex(root_lex<true, kExact>(g0, g1, o, d, a, tr.tb, tr.tb * kCullScale), bid[k], tr.tb, tr.best);
     }
-    if (false)
-#endif
-    for (int k = 0; k < A.n_big; ++k)
-#if PTG_BEST_LEAF
-        update_lex_c(A, root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb, tr.tb * kCullScale),
-                     -2 - k, tr.tb, tr.best);
-#else
-        update_lex(root_lex<true, kExact>(A.big_geo[k].g0, A.big_geo[k].g1, o, d, a, tr.tb, tr.tb * kCullScale),
-                   A.big_id[k], tr.tb, tr.best);
-#endif
     if constexpr (kCount)
         cnt.spheres += A.n_big;
-#if PTG_BVH_WIDE
     // the wide layouts store each box near-plane first for their octant:
     // all 8 layouts exist (bvh_oct_mask = 7)
-#if PTG_BVH_ONE_LAYOUT
-    tr.ni = A.n_nodes > 0 ? 0 : -1;  // the one layout, for every octant
-#else
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
-#if PTG_BVH_INTERLEAVE
     tr.ni = A.n_nodes > 0 ? (int)(oct << 2) : -1;  // layout k's root: interleaved node k
-#else
-    // layout k at record k * (2^shift + PTG_BVH_LAYOUT_PAD)
-    tr.ni = A.n_nodes > 0 ? (int)((oct << A.bvh_shift) + oct * PTG_BVH_LAYOUT_PAD) : -1;
-#endif
-#endif
     tr.s0 = -1;
     tr.s1 = -1;
 #if PTG_BVH_STACK >= 3
@@ -1371,13 +873,6 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 #endif
     tr.res = -1;
     (void)oct_mask;
-#elif PTG_BVH_OCTANTS
-    const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
-                         ((__float_as_uint(d.z) >> 29) & 4u);
-    tr.ni = (int)((oct & (unsigned)oct_mask) << A.bvh_shift);
-#else
-    tr.ni = 0;
-#endif
     tr.pend = -1;
 }
 
@@ -1387,39 +882,6 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
 struct SlabRay {
     float sx, sy, sz, bx, by, bz;
 };
-#if PTG_BVH_ONE_LAYOUT
-// The one layout stores each child box min-plane first: words {x0, y0},
-// {z0, x1}, {y1, z1} (low half first).  Per lane and axis one v_perm_b32
-// gathers the axis's two planes into one word, near plane in the low half:
-// for d_k >= 0 the min plane, else the max plane.  Selector bytes index
-// {S0, S1} as S1 = 0..3, S0 = 4..7.
-//   x: S0 = w0 (x0 at 4,5), S1 = w1 (x1 at 2,3)  -> {x0, x1} 0x03020504, {x1, x0} 0x05040302
-//   y: S0 = w0 (y0 at 6,7), S1 = w2 (y1 at 0,1)  -> {y0, y1} 0x01000706, {y1, y0} 0x07060100
-//   z: S0 = w1 (z0 at 4,5), S1 = w2 (z1 at 2,3)  -> {z0, z1} 0x03020504, {z1, z0} 0x05040302
-// The selector is a bitfield insert on the sign mask of the slab scale
-// (sign of d_k): 2 VALU per axis per node step, kept out of the walk's
-// registers.
-__device__ __forceinline__ unsigned near_sel(float s, unsigned pos, unsigned neg)
-{
-    const unsigned m = (unsigned)(__float_as_int(s) >> 31);  // all ones for d_k < 0
-    return (m & neg) | (~m & pos);  // v_bfi_b32
-}
-__device__ __forceinline__ bool box_hit_one(const u32x4 q, const SlabRay &r, const float tcap)
-{
-    const unsigned px = __builtin_amdgcn_perm(q.x, q.y, near_sel(r.sx, 0x03020504u, 0x05040302u));
-    const unsigned py = __builtin_amdgcn_perm(q.x, q.z, near_sel(r.sy, 0x01000706u, 0x07060100u));
-    const unsigned pz = __builtin_amdgcn_perm(q.y, q.z, near_sel(r.sz, 0x03020504u, 0x05040302u));
-    const float tnx = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(px & 0xFFFFu)), r.sx, r.bx);
-    const float tny = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(py & 0xFFFFu)), r.sy, r.by);
-    const float tnz = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(pz & 0xFFFFu)), r.sz, r.bz);
-    const float tfx = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(px >> 16)), r.sx, r.bx);
-    const float tfy = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(py >> 16)), r.sy, r.by);
-    const float tfz = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(pz >> 16)), r.sz, r.bz);
-    const float t_in = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, 0.0f));
-    const float t_out = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, tcap));
-    return !(t_in > t_out);
-}
-#endif
 __device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
 {
     const float ix = d.x != 0.0f ? __builtin_amdgcn_rcpf(d.x) : __builtin_copysignf(1e30f, d.x);
@@ -1435,26 +897,7 @@ __device__ __forceinline__ SlabRay slab_ray(const KArgs &A, f3 o, f3 d)
     return r;
 }
 
-#if !PTG_BVH_WIDE
-// Box test of one compact record (culling only): slab entry/exit in grid
-// units, padded.
-__device__ __forceinline__ bool box_hit(const u32x4 q, const SlabRay &r, const float tcap)
-{
-    const float tx1 = __builtin_fmaf((float)(q.x & 0xFFFFu), r.sx, r.bx);
-    const float ty1 = __builtin_fmaf((float)(q.x >> 16), r.sy, r.by);
-    const float tz1 = __builtin_fmaf((float)(q.y & 0xFFFFu), r.sz, r.bz);
-    const float tx2 = __builtin_fmaf((float)(q.y >> 16), r.sx, r.bx);
-    const float ty2 = __builtin_fmaf((float)(q.z & 0xFFFFu), r.sy, r.by);
-    const float tz2 = __builtin_fmaf((float)(q.z >> 16), r.sz, r.bz);
-    const float t_in = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
-                                       __builtin_fmaxf(__builtin_fminf(tz1, tz2), 0.0f));
-    const float t_out = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
-                                        __builtin_fminf(__builtin_fmaxf(tz1, tz2), tcap));
-    return !(t_in > t_out * 1.0001f + 1e-6f);
-}
-#endif
 
-#if PTG_BVH_WIDE
 // Box test of a wide-layout record: binary16 planes on the wide grid, stored
 // near-plane first for the ray's octant (bvh_build.hpp WideGrid), each read
 // by one v_fma_mix_f32.  No slab margin: the boxes are padded far beyond the
@@ -1488,9 +931,7 @@ __device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, 
 // when a leaf was parked: ni = kPopLater then, and the leaf phase pops.
 // Selections are branch-free (v_cndmask).
 constexpr int kPopLater = -2;
-#if PTG_LEAF_DONE_SEL
 __device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bool need, const int keep);
-#endif
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r_in, BvhTrav &tr,
                                               ScanCount &cnt, const u32x4 *lds_root = nullptr, int root_mask = 0,
@@ -1498,70 +939,23 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
 {
     const int base = tr.ni & ~3;
     u32x4 q0, q1, q2, q3;
-#if PTG_BVH_Q8
-    const SlabRay &r0 = r_in;
-    // 48-B node (bvh_build.hpp wide_q8) at byte 12 base: the words, the
-    // node's grid (binary16 origin in 256-step units, step exponents) and the
-    // 24 plane bytes, read as subnormal binary16 halves q 2^-24 by the box
-    // tests' v_fma_mix_f32: per axis t = h S + B with S = sx 2^(F + 8)
-    // (sx = 256 q_scale / d: sx 2^(E + 24)) and B = origin sx + bx
-    gptr<u32x4> qq = (gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + (unsigned)base * (PTG_BVH_Q8_STRIDE / 4u));
-    const u32x4 W = qq[0], Hd = qq[1], Pd = qq[2];
-    SlabRay r;
-    r.sx = __builtin_amdgcn_ldexpf(r0.sx, (int)__builtin_amdgcn_ubfe(Hd.y, 16, 5));
-    r.sy = __builtin_amdgcn_ldexpf(r0.sy, (int)__builtin_amdgcn_ubfe(Hd.y, 21, 5));
-    r.sz = __builtin_amdgcn_ldexpf(r0.sz, (int)__builtin_amdgcn_ubfe(Hd.y, 26, 5));
-    r.bx = __builtin_fmaf(lo_half(Hd.x), r0.sx, r0.bx);
-    r.by = __builtin_fmaf(hi_half(Hd.x), r0.sy, r0.by);
-    r.bz = __builtin_fmaf(lo_half(Hd.y), r0.sz, r0.bz);
-    // a dword's pairs: bytes (0, 2) and (1, 3) as the halves' low bytes
-    auto pe = [](unsigned d) { return d & 0x00FF00FFu; };
-    auto po = [](unsigned d) { return __builtin_amdgcn_perm(d, d, 0x0C030C01u); };
-    q0 = u32x4{pe(Hd.z), po(Hd.z), pe(Hd.w), W.x};
-    q1 = u32x4{po(Hd.w), pe(Pd.x), po(Pd.x), W.y};
-    q2 = u32x4{pe(Pd.y), po(Pd.y), pe(Pd.z), W.z};
-    q3 = u32x4{po(Pd.z), pe(Pd.w), po(Pd.w), W.w};
-    (void)lds_root;
-    (void)root_mask;
-    (void)shift;
-#else
     const SlabRay &r = r_in;
-#if PTG_BVH_LDS_ROOT
-    if (lds_root && (base & root_mask) == 0) {  // a layout's root: staged in LDS
-        const u32x4 *l = lds_root + ((base >> shift) << 2);
-        q0 = l[0];
-        q1 = l[1];
-        q2 = l[2];
-        q3 = l[3];
-    } else
-#endif
     {
-#if PTG_NODE_OFS32
         // a 32-bit byte offset on the uniform base: the load's saddr form
         // (no 64-bit address arithmetic per lane)
         gptr<u32x4> q = (gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + ((unsigned)base << 4));
-#else
-        gptr<u32x4> q = qnodes + base;
-#endif
         q0 = q[0];
         q1 = q[1];
         q2 = q[2];
         q3 = q[3];
     }
-#endif
     if constexpr (kCount)
         cnt.boxes += 4 - (tr.ni & 3);
     const float tcap = tr.tb * 1.0001f;
-#if PTG_NODE_CASCADE
     // slots before the walk's position (ni & 3) are not tested again
     const int s = tr.ni & 3;
-#if PTG_BVH_ONE_LAYOUT
-    const bool h0 = box_hit_one(q0, r, tcap) & (s == 0), h1 = box_hit_one(q1, r, tcap) & (s <= 1),
-               h2 = box_hit_one(q2, r, tcap) & (s <= 2), h3 = box_hit_one(q3, r, tcap);
-#else
     const bool h0 = box_hit_sorted(q0, r, tcap) & (s == 0), h1 = box_hit_sorted(q1, r, tcap) & (s <= 1),
                h2 = box_hit_sorted(q2, r, tcap) & (s <= 2), h3 = box_hit_sorted(q3, r, tcap);
-#endif
     // the words of the first three hits in slot order (-1: none) and the
     // slots of the second and third, shifted in from the last slot: every
     // step is a v_cndmask on its box test's lane mask (the hit mask with
@@ -1591,30 +985,7 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     const bool push = leaf ? w3 != -1 : w2 != -1;
     const int pos = base + (leaf ? i3 : i2);
     const int e = leaf ? ((h0 & h1 & h2 & h3) ? pos : w3) : (w3 != -1 ? pos : w2);
-#else
-    const unsigned m = ((box_hit_sorted(q0, r, tcap) ? 1u : 0u) | (box_hit_sorted(q1, r, tcap) ? 2u : 0u) |
-                        (box_hit_sorted(q2, r, tcap) ? 4u : 0u) | (box_hit_sorted(q3, r, tcap) ? 8u : 0u)) &
-                       (0xFu << (tr.ni & 3));
-    // the word of the lowest set bit of x (x != 0)
-    auto lowest = [&](unsigned x) {
-        int w = (int)q3.w;
-        w = (x & 4u) ? (int)q2.w : w;
-        w = (x & 2u) ? (int)q1.w : w;
-        return (x & 1u) ? (int)q0.w : w;
-    };
-    const unsigned r1 = m & (m - 1u);  // hits after the first
-    const int wf = lowest(m), ws = lowest(r1);
-    const bool leaf = (m != 0u) & (wf < kPopLater);  // the first hit is a leaf: parked
-    const unsigned rest = leaf ? r1 & (r1 - 1u) : r1;
-    int next = m == 0u ? -1 : leaf ? (r1 != 0u ? ws : kPopLater) : wf;
-    tr.pend = leaf ? (wf & 0x7FFFFFFF) : tr.pend;
-    const int pos = base + (int)__builtin_ctz(rest | 16u);
-    const int e = (rest & (rest - 1u)) != 0u ? pos : lowest(rest);
-#endif
 #if PTG_BVH_STACK >= 3
-#if !PTG_NODE_CASCADE
-    const bool push = rest != 0u;
-#endif
     const bool full = tr.s2 != -1;
     tr.res = (push & full) ? pos : tr.res;
     const int s0 = tr.s0, s1 = tr.s1;
@@ -1622,24 +993,12 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
     tr.s1 = push ? (full ? -1 : s0) : s1;
     tr.s2 = push ? (full ? -1 : s1) : tr.s2;
 #else
-#if !PTG_NODE_CASCADE
-    const bool push = rest != 0u;
-#endif
     const bool full = tr.s1 != -1;
     tr.res = (push & full) ? pos : tr.res;
     const int s0 = tr.s0;
     tr.s0 = push ? (full ? -1 : e) : s0;
     tr.s1 = push ? (full ? -1 : s0) : tr.s1;
 #endif
-#if PTG_NODE_POP_SEL && PTG_LEAF_DONE_SEL
-    // the pop as selects for every stepping lane (bvh_pop_sel, as the leaf
-    // completion): no divergent branch whose join copies the stack registers
-    const bool need = next == -1;
-    next = bvh_pop_sel(cont, tr, need, next);
-    const bool lf = need & (next < kPopLater);  // a leaf from the stack
-    tr.pend = lf ? (next & 0x7FFFFFFF) : tr.pend;
-    next = lf ? kPopLater : next;
-#else
     if (next == -1) {
         next = bvh_pop(cont, tr);
         if (next < kPopLater) {  // a leaf from the stack
@@ -1647,11 +1006,9 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
             next = kPopLater;
         }
     }
-#endif
     tr.ni = next;
 }
 
-#if PTG_LEAF_DONE_SEL
 // The render kernel's leaf completion (bvh_leaf_done) and its pop, executed
 // by every lane of the wave: lanes without a tested leaf (act false) keep
 // their state through selects.  As nested divergent branches the update
@@ -1689,23 +1046,6 @@ __device__ __forceinline__ void bvh_leaf_done_sel(gptr<int> cont, BvhTrav &tr, c
     next = lf ? kPopLater : next;
     tr.ni = act ? next : tr.ni;
 }
-#endif
-#else
-// One node step: test node tr.ni's box; hit -> descend (ni + 1; a leaf is
-// parked in tr.pend), miss -> skip the subtree.
-template <bool kCount>
-__device__ __forceinline__ void bvh_node_step(gptr<int>, gptr<u32x4> qnodes, const SlabRay &r, BvhTrav &tr,
-                                              ScanCount &cnt)
-{
-    const u32x4 q = qnodes[tr.ni];  // one 16-B load
-    if constexpr (kCount)
-        cnt.boxes += 1;
-    const bool hit = box_hit(q, r, tr.tb * 1.0001f);
-    const int w = (int)q.w;  // >= 0 inner node's skip; < 0 leaf (its skip is the next node)
-    tr.pend = (hit && w < 0) ? (w & 0x7FFFFFFF) : -1;
-    tr.ni = (hit || w < 0) ? tr.ni + 1 : w;
-}
-#endif
 
 // Spheres [f, f + cnt) of the leaf order against one ray: compact records
 // {C, -R^2}; (tb, best) updated by the lex rule.
@@ -1716,46 +1056,19 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
     const float a = dot3(d, d);
     if constexpr (kCount)
         sc.spheres += cnt;
-#if PTG_NODE_OFS32
     // 32-bit byte offsets on the uniform bases (saddr loads)
     const char *sph = (const char *)A.bvh_sph;
     const char *ids = (const char *)A.bvh_id;
     float tbm = tb * kCullScale;
     for (int j = 0; j < cnt; ++j) {
         const unsigned off = (unsigned)(f + j) << 4;
-#if PTG_LEAF_NT
-        // non-temporal: the leaf records stream past the L1, whose lines
-        // then hold the walk's upper node levels (A/B)
-        typedef float f32x4 __attribute__((ext_vector_type(4)));
-        const f32x4 v = __builtin_nontemporal_load((const f32x4 *)(sph + off));
-        const float4 rec = make_float4(v.x, v.y, v.z, v.w);
-#else
         const float4 rec = *(const float4 *)(sph + off);
-#endif
         const float t = root_lex<false, kExact>(rec, float4{}, o, d, a, tb, tbm);
-#if PTG_LEAF_NOBRANCH && !PTG_BEST_LEAF
-        update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
-        tbm = tb * kCullScale;
-        if (false) {
-#else
         if (t <= tb) {  // the scene index is read only for a candidate that wins or ties
-#endif
-#if PTG_BEST_LEAF
-            (void)ids;
-            update_lex_c(A, t, f + j, tb, best);
-#else
             update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
-#endif
             tbm = tb * kCullScale;
         }
     }
-#else
-    for (int j = 0; j < cnt; ++j) {
-        const float t = root_lex<false, kExact>(A.bvh_sph[f + j], float4{}, o, d, a, tb, tb * kCullScale);
-        if (t <= tb)  // the scene index is read only for a candidate that wins or ties
-            update_lex(t, A.bvh_id[f + j], tb, best);
-    }
-#endif
 }
 
 // After the parked leaf's spheres: wide walk -- a leaf word waiting in tr.ni
@@ -1763,7 +1076,6 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
 __device__ __forceinline__ void bvh_leaf_done(gptr<int> cont, BvhTrav &tr)
 {
     tr.pend = -1;
-#if PTG_BVH_WIDE
     if (tr.ni < -1) {  // kPopLater, or the leaf the node step moved to after parking one
         int next = tr.ni == kPopLater ? bvh_pop(cont, tr) : tr.ni;
         if (next < kPopLater) {  // a leaf: parked for the next leaf phase
@@ -1772,9 +1084,6 @@ __device__ __forceinline__ void bvh_leaf_done(gptr<int> cont, BvhTrav &tr)
         }
         tr.ni = next;
     }
-#else
-    (void)cont;
-#endif
 }
 
 // The parked leaf's spheres, all by this lane.
@@ -1782,12 +1091,7 @@ template <bool kCount, bool kExact>
 __device__ __forceinline__ void bvh_leaf(const KArgs &A, gptr<int> cont, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
     const int first = tr.pend & 0xFFFFFF, nl = tr.pend >> 24;
-#if PTG_LEAF_CHUNK > 0
-    // at most PTG_LEAF_CHUNK spheres per leaf phase; the rest stays parked
-    const int take = nl < PTG_LEAF_CHUNK ? nl : PTG_LEAF_CHUNK;
-#else
     const int take = nl;
-#endif
     leaf_spheres<kCount, kExact>(A, first, take, o, d, tr.tb, tr.best, cnt);
     if (take < nl) {
         tr.pend = (first + take) | ((nl - take) << 24);
@@ -1876,25 +1180,12 @@ __device__ __forceinline__ void bvh_leaf_split(const KArgs &A, gptr<int> cont, f
     const float htb = bpf(partner, tb), htb2 = bpf(partner2, tb);
     const int hbest = bpi(partner, best), hbest2 = bpi(partner2, best);
     if (po) {
-#if PTG_BEST_LEAF
-        update_lex_c(A, htb, hbest, tb, best);
-        update_lex_c(A, htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
-#else
         update_lex(htb, hbest, tb, best);
         update_lex(htb2, hbest2, tb, best);  // partner2 = lane without a second helper: a no-op
-#endif
     }
-#if PTG_BVH_WIDE && PTG_LEAF_DONE_SEL
     tr.tb = has ? tb : tr.tb;
     tr.best = has ? best : tr.best;
     bvh_leaf_done_sel(cont, tr, has);
-#else
-    if (has) {
-        tr.tb = tb;
-        tr.best = best;
-        bvh_leaf_done(cont, tr);
-    }
-#endif
 }
 
 // Whole scan of one ray (parity probe kernel): walk, testing each parked leaf
@@ -1912,11 +1203,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
             bvh_node_step<kCount>((gptr<int>)A.bvh_cont, (gptr<u32x4>)A.bvh_qnodes, sr, tr, cnt);
     }
     tbest = tr.tb;
-#if PTG_BEST_LEAF
-    return sid_of(A, tr.best);
-#else
     return tr.best;
-#endif
 }
 
 // Per-lane state machine: one call = one bounce segment of radiance()
@@ -1924,7 +1211,7 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
 // its radiance.
 // shade(): everything after the scene scan -- sky on a miss, else hit
 // record, emission, Russian roulette, BRDF sampling of the next ray.
-template <bool kExact, bool kPacked = false>
+template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st);
 
@@ -1941,19 +1228,17 @@ __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, cons
         const LinRec *w = scene_scan<kExact>(A, recs, o, d, t);
         hit = w != recs + A.n ? &w->s : nullptr;
     }
-    return shade<kExact, kBvh && PTG_SHADE_PACK>(hit, t, trig, o, d, T, E, depth, st);
+    return shade<kExact>(hit, t, trig, o, d, T, E, depth, st);
 }
 
-template <bool kExact, bool kPacked>
+template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st)
 {
-#if PTG_DEPTH_EARLY
     // the segment count first, for every lane: a sky lane's path ends here
     // (its depth is reset by the refill), so the value is only read below --
     // no per-branch copy of the loop-carried register
     depth += 1;
-#endif
     if (!hit) {  // main.cpp:115-120: sky
         f3 ud = norm3m<kExact>(d);
         float tt = 0.5f * (ud.y + 1.0f);
@@ -1965,32 +1250,17 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     }
     const ShadeRec &S = *hit;
     float4 s0 = S.s0;
-    [[maybe_unused]] float4 s1;
-    if constexpr (!kPacked)
-        s1 = S.s1;
-#if PTG_SHADE_EARLY
-    // the record's reads issued first, the roulette's draw (independent of
-    // them) computed while they are in flight -- held there by a scheduling
-    // barrier
-    const float4 c2 = S.s2, c3 = S.s3;
-    uint32_t st_rr = st;
-    const uint32_t m_rr = draw_bits(st_rr);
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    const float4 s1 = S.s1;
     // hit_record.cpp:3-12
     f3 p = mk3(__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z));
     // hit_record.cpp:6 (p - C).norm() as (p - C) * (1/R): p lies on the sphere
-#if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
-    const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
+    const bool rr = depth > kRRThreshold + 1;  // (the depth before this segment's count)
     const float4 cc = *(rr ? &S.s3 : &S.s2);  // (prepare_scene: 1/R in s2.w and s3.w)
     const float invR = cc.w;
-#else
-    const float invR = S.s2.w;
-#endif
     bool front;
     f3 on, nn;
-    [[maybe_unused]] float kn = 0.0f;  // PTG_FAST_NN: nn.d
-    if (PTG_FAST_NN && !kExact) {
+    [[maybe_unused]] float kn = 0.0f;  // fast mode: nn.d
+    if (!kExact) {
         const f3 pc = mk3(p.x - s0.x, p.y - s0.y, p.z - s0.z);
         const float sd = dot3(pc, d);
         front = sd < 0.0f;
@@ -2004,56 +1274,26 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         nn = front ? on : mk3(-on.x, -on.y, -on.z);
     }
     // main.cpp:126
-    if constexpr (kPacked) {
-        // (PTG_SHADE_PACK: s0.w bit 30 = the sphere emits; its emission read here)
-        if (__float_as_uint(s0.w) >> 30) {
-            const float4 em = S.s1;
-            E = mk3(__builtin_fmaf(T.x, em.x, E.x), __builtin_fmaf(T.y, em.y, E.y), __builtin_fmaf(T.z, em.z, E.z));
-        }
-    } else {
-        E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
-    }
-    // main.cpp:128-139: Russian roulette after depth 4 (PTG_RR_ROWSEL: the
-    // colour row read above by address; else both rows read and selected)
-#if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
-#elif !PTG_SHADE_EARLY
-    const float4 c2 = S.s2, c3 = S.s3;
-    const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
-#else
-    const bool rr = depth > kRRThreshold + PTG_DEPTH_EARLY;  // (the depth before this segment's count)
-#endif
+    E = mk3(__builtin_fmaf(T.x, s1.x, E.x), __builtin_fmaf(T.y, s1.y, E.y), __builtin_fmaf(T.z, s1.z, E.z));
+    // main.cpp:128-139: Russian roulette after depth 4 (the colour row read
+    // above by address)
     // Russian roulette without an early return: the roulette's draw advances the state of the
     // rr lanes only (a select), and a killed lane runs on with its materials
     // masked -- its next ray and state are discarded (the early return's
     // merge had cost state copies and exec-mask blocks)
-#if !PTG_SHADE_EARLY
     uint32_t st_rr = st;
-#endif
-#if PTG_RR_INT
-#if !PTG_SHADE_EARLY
     const uint32_t m_rr = draw_bits(st_rr);  // u = m_rr 2^-24; s0.w holds ceil(p 2^24) (prepare_scene)
-#endif
     st = rr ? st_rr : st;
-    const bool killed = rr & !(m_rr < (kPacked ? (__float_as_uint(s0.w) & 0x1FFFFFFu) : __float_as_uint(s0.w)));
-#else
-    const float u_rr = draw(st_rr);
-    st = rr ? st_rr : st;
-    const bool killed = rr & !(u_rr < s0.w);  // (box -0.6 %, box_mirror -1.0 %)
-#endif
-#if PTG_RR_ROWSEL && !PTG_SHADE_EARLY
+    const bool killed = rr & !(m_rr < __float_as_uint(s0.w));
     T = mk3(T.x * cc.x, T.y * cc.y, T.z * cc.z);
-#else
-    T = mk3(T.x * (rr ? c3.x : c2.x), T.y * (rr ? c3.y : c2.y), T.z * (rr ? c3.z : c2.z));
-#endif
     // BRDF samplers (main.cpp:44-97).  Diffuse and dielectric lanes share the
     // three expensive ops (one rsqrt, two sqrt) through selects, so a wave
     // holding both materials issues them once; every lane's arithmetic is the
     // same as the per-material code (oracle sample_B).
-    const int mat = kPacked ? (int)((__float_as_uint(s0.w) >> 28) & 3u) : __float_as_int(s1.w);
+    const int mat = __float_as_int(s1.w);
     const bool isD = !killed & (mat == PTG_DIFFUSE);
     const bool isG = !killed & (mat == PTG_DIELECTRIC);
     bool spec = !killed & (mat == PTG_SPECULAR);
-#if PTG_DRAW_MERGE
     // every lane's first BRDF draw taken once, here: the diffuse phi, the
     // dielectric's Fresnel draw -- or, where it cannot refract, its
     // reflection's draw -- and the mirror's draw (main.cpp:46, :89, :62).
@@ -2062,98 +1302,32 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     // killed lanes advance a state their ended path no longer reads.
     const uint32_t m1 = draw_bits(st);
     [[maybe_unused]] bool fres = false;
-#if PTG_U1_HOIST
     // its value u = m1 2^-24, converted once for the diffuse phi (fast
     // mode: v_sin / v_cos take revolutions) and the Fresnel compare
     const float u1 = (float)m1 * 0x1p-24f;
-#endif
-#if PTG_DRAW2_MERGE
-    // and every lane's second draw, taken here too: the diffuse r, and the
-    // reflection's draw of a dielectric lane reflected by its Fresnel draw
-    // (its value unused, main.cpp:62); the state after it is kept only by
-    // those lanes (st2, committed after the samplers)
-    uint32_t st2 = st;
-    const uint32_t m2 = draw_bits(st2);
-#endif
-#endif
-#if PTG_D_INPLACE
-    // the next direction written into d in place: each lane's sampler writes
-    // it after the lane's last read of d (a refraction only where no
-    // reflection follows), so the loop-carried register needs no copy
-    f3 &nd = d;
-#else
     f3 nd = d;  // every lane sets it below (mirror lanes in the spec block)
-#endif
     // a wave with only mirror lanes skips the diffuse/dielectric work
     // (wave-uniform, exact: those lanes' values are all overwritten)
-#if PTG_DG_SKIP
     // (the ballot of one compare, free from its lane mask: a ballot of
     // isD | isG was materialised as v_cndmask + v_cmp; killed lanes of
     // those materials run the block for nothing, their values unused)
     if (__ballot(mat != PTG_SPECULAR) != 0ull)
-#endif
     {
         PTG_STAT(4);
 #if PTG_BLOCK_STATS == 3  // debug: wave cycles of the diffuse/dielectric block in [14]
         const unsigned long long dg_t0 = clock64();
 #endif
-#if PTG_DG_SPLIT
-        // a wave without dielectric lanes runs the diffuse sampler alone:
-        // the same operations for every diffuse lane as the shared code
-        // below (bit for bit), without the dielectric half of its selects
-        // and the refraction vector (wave-uniform, exact)
-        if (__ballot(isG) == 0ull) {
-            if (isD) {
-#if PTG_DRAW_MERGE
-                const uint32_t m_phi = m1;
-#else
-                const uint32_t m_phi = draw_bits(st);
-#endif
-#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
-                const float ra = (float)m2 * 0x1p-24f;
-#else
-                const float ra = draw(st);
-#endif
-                float cp, sp;
-                Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
-                const f3 uu = __builtin_fabsf(nn.x) > 0.1f ? mk3(nn.z, 0.0f, -nn.x) : mk3(0.0f, -nn.z, nn.y);
-                const float r1 = Math<kExact>::rsqrt(dot3(uu, uu));
-                const f3 v1 = mk3(uu.x * r1, uu.y * r1, uu.z * r1);
-                const float s2 = Math<kExact>::sqrt0(ra);
-                const float s3 = Math<kExact>::sqrt(1.0f - ra);
-                const f3 vv = cross3(nn, v1);
-                const float cs = cp * s2, ss = sp * s2;
-                nd = mk3(__builtin_fmaf(nn.x, s3, __builtin_fmaf(vv.x, ss, v1.x * cs)),
-                         __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
-                         __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
-            }
-        } else
-#endif
         {
-#if PTG_DG_NOINIT
         // read only where isD (the ?: operands and the isD branch below):
         // no initial values to set for the other lanes
         float cp, sp, ra;
-#else
-        float cp = 0.0f, sp = 0.0f, ra = 0.0f;
-#endif
         if (isD) {  // main.cpp:46-47: phi = 2 pi u, r = u
-#if PTG_DRAW_MERGE
             const uint32_t m_phi = m1;
-#else
-            const uint32_t m_phi = draw_bits(st);
-#endif
-#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
-            ra = (float)m2 * 0x1p-24f;  // draw()'s value of m2
-#else
             ra = draw(st);
-#endif
-#if PTG_U1_HOIST
             if constexpr (!kExact) {
                 cp = __builtin_amdgcn_cosf(u1);  // Math<false>::sincos2pi of m1
                 sp = __builtin_amdgcn_sinf(u1);
             } else
-#endif
             Math<kExact>::sincos2pi(m_phi, trig, cp, sp);
         }
         // op1: diffuse -> u = norm((|w.x| > 0.1 ? y : x) x w) (main.cpp:52); dielectric -> norm(d) (main.cpp:75)
@@ -2162,12 +1336,8 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         const float r1 = Math<kExact>::rsqrt(dot3(v1, v1));
         v1 = mk3(v1.x * r1, v1.y * r1, v1.z * r1);
         const float x0 = -dot3(v1, nn);
-#if PTG_CTH_MIN
         // fast mode: one v_min_f32 (differs from the select only for NaN)
         const float cthG = kExact ? (1.0f < x0 ? 1.0f : x0) : __builtin_fminf(1.0f, x0);  // main.cpp:77
-#else
-        const float cthG = 1.0f < x0 ? 1.0f : x0;  // main.cpp:77
-#endif
         // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
         const float s2 = Math<kExact>::sqrt0(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
         const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
@@ -2179,23 +1349,13 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
                 float x2 = xm * xm;
                 float x5 = (x2 * x2) * xm;
                 float R = __builtin_fmaf(1.0f - r0, x5, r0);
-#if PTG_DRAW_MERGE
-#if PTG_U1_HOIST
                 reflect = R > u1;
-#else
-                reflect = R > (float)m1 * 0x1p-24f;  // draw()'s value of m1
-#endif
                 fres = true;
-#if PTG_FRES_IN_BLOCK
                 {  // the reflection's draw right after the Fresnel draw that chose it
                     uint32_t st2 = st;
                     (void)draw_bits(st2);
                     st = reflect ? st2 : st;
                 }
-#endif
-#else
-                reflect = R > draw(st);
-#endif
             }
             spec = reflect;
         }
@@ -2210,9 +1370,6 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
                      __builtin_fmaf(nn.y, s3, __builtin_fmaf(vv.y, ss, v1.y * cs)),
                      __builtin_fmaf(nn.z, s3, __builtin_fmaf(vv.z, ss, v1.z * cs)));
         } else
-#if PTG_D_INPLACE
-        if (!spec)
-#endif
         {  // refraction, main.cpp:93-96
             nd = mk3(__builtin_fmaf(nn.x, -s3, perp.x), __builtin_fmaf(nn.y, -s3, perp.y),
                      __builtin_fmaf(nn.z, -s3, perp.z));
@@ -2228,33 +1385,15 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     }
     if (spec) {  // main.cpp:60-67 (fuzz draw consumed, multiplied by 0)
         PTG_STAT(5);
-        // (PTG_FAST_NN: on the facing normal nn = +-on, its dot kn)
-        float k = (PTG_FAST_NN && !kExact) ? kn : dot3(on, d);
+        // (fast mode: on the facing normal nn = +-on, its dot kn)
+        float k = !kExact ? kn : dot3(on, d);
         k = k + k;
-#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
-        // (the reflection's draw after a Fresnel draw: st2, committed below)
-#elif PTG_DRAW_MERGE && PTG_FRES_IN_BLOCK
         // (the reflection's draw after a Fresnel draw: taken in the Fresnel block)
-#elif PTG_DRAW_MERGE
-        {  // the reflection's draw after a Fresnel draw (the others took m1)
-            uint32_t st2 = st;
-            (void)draw_bits(st2);
-            st = fres ? st2 : st;
-        }
-#else
-        (void)draw(st);
-#endif
-        const f3 rn = (PTG_FAST_NN && !kExact) ? nn : on;
+        const f3 rn = !kExact ? nn : on;
         nd = mk3(__builtin_fmaf(-k, rn.x, d.x), __builtin_fmaf(-k, rn.y, d.y), __builtin_fmaf(-k, rn.z, d.z));
     }
-#if PTG_DRAW_MERGE && PTG_DRAW2_MERGE
-    st = (isD | (fres & spec)) ? st2 : st;
-#endif
     o = p;
     d = nd;
-#if !PTG_DEPTH_EARLY
-    depth += 1;
-#endif
     return killed | (depth >= kDepthLimit);
 }
 
@@ -2312,15 +1451,13 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     // on its node loads) reads it from global memory (L1): measured the same
     const float2 *trig = A.trig;
     if constexpr (kLdsGeo) {
-#if PTG_TRIG_LDS
         if constexpr (kExact) {  // (the fast mode's v_sin/v_cos need no table)
             __shared__ float2 lds_trig[kTrigEntries];
             for (int i = threadIdx.x; i < kTrigEntries; i += kBlock)
                 lds_trig[i] = A.trig[i];
             trig = lds_trig;
         }
-#endif
-        for (int i = threadIdx.x; i <= A.n + 1 + 2 * PTG_WALL_GEO; i += kBlock)  // n records + the sentinel + the wall table(s)
+        for (int i = threadIdx.x; i <= A.n + 1 + 2; i += kBlock)  // n records + the sentinel + the wall table(s)
             lds_lin[i] = A.lin[i];
         recs = lds_lin;
     }
@@ -2525,19 +1662,11 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         parked = false;
     };
     // path end: park the radiance and start the prefetched ray, or wait
-    [[maybe_unused]] float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pq1 = pq0;  // PTG_PRE_EARLY
     auto path_done = [&]() {
         item = -1;
         if (has_pre) {
             const float4 *rec = pre_rec();
-            float4 p0, p1;
-            if (PTG_PRE_EARLY && !kBvh) {
-                p0 = pq0;
-                p1 = pq1;
-            } else {
-                p0 = rec[0];
-                p1 = rec[1];
-            }
+            const float4 p0 = rec[0], p1 = rec[1];
             park();
             begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
             has_pre = false;
@@ -2640,28 +1769,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
-                if constexpr (PTG_PRE_EARLY && !kBvh) {
-                    const float4 *rec = pre_rec();
-                    pq0 = rec[0];
-                    pq1 = rec[1];
-                }
                 if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
                     path_done();
             }
             refill();
-#if PTG_LIN_UNROLL2
-            // the loop body twice: the two copies can hold the ray's
-            // loop-carried registers in alternating places (no join copies)
-            if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
-                break;
-            if (item >= 0) {
-                if constexpr (kCount)
-                    segs += 1;
-                if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
-                    path_done();
-            }
-            refill();
-#endif
 #endif
         }
 #if PTG_BLOCK_STATS == 3
@@ -2678,17 +1789,6 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
 #if PTG_LEAF_SPLIT
         __shared__ uint8_t lds_pair[kWaves][2][64];  // leaf phase: owner / helper lane of each rank
 #endif
-#if PTG_BVH_LDS_ROOT
-        // the 8 octant layouts' root nodes (4 records each), 512 B
-        __shared__ u32x4 lds_root[8][4];
-        int root_shift = A.bvh_shift;
-        asm volatile("" : "+s"(root_shift));
-        const int root_mask = (1 << root_shift) - 1;
-        if (A.n_nodes > 0 && lane < 32)
-            lds_root[lane >> 2][lane & 3] = ((gptr<u32x4>)A.bvh_qnodes)[((lane >> 2) << root_shift) + (lane & 3)];
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_wave_barrier();
-#endif
         // kernel-argument pointers used in the loops, pinned in SGPRs once:
         // left to the compiler they were re-loaded (s_load + wait) in every
         // node step and every shade
@@ -2696,16 +1796,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         asm volatile("" : "+s"(qnodes));
         gptr<int> cont = (gptr<int>)A.bvh_cont;
         asm volatile("" : "+s"(cont));
-#if !PTG_NO_TRIG_PIN
         if constexpr (kExact)  // (the fast mode's sin/cos read no table)
             asm volatile("" : "+s"(trig));
-#endif
-#if PTG_BVH_WIDE
         const int oct_mask = 7;  // every octant has its layout
-#else
-        int oct_mask = A.bvh_oct_mask;
-        asm volatile("" : "+s"(oct_mask));
-#endif
 #if PTG_BLOCK_STATS == 2
         unsigned long long ph_cyc[6] = {0, 0, 0, 0, 0, 0}, ph_t = clock64();
 #endif
@@ -2754,12 +1847,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         // (the node step as selects for the whole wave, like the
                         // leaf completion: +2.3 % -- its loads and selects for idle lanes)
                         if (trv && tr.pend < 0)
-#if PTG_BVH_LDS_ROOT
-                            bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt, &lds_root[0][0],
-                                                                     root_mask, root_shift);
-#else
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
-#endif
                         PTG_PHASE(1);
                         phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
                     }
@@ -2790,16 +1878,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             PTG_PHASE(5);
             if (item >= 0 && phase == 2) {
                 phase = 0;
-#if PTG_BEST_LEAF && PTG_SHADE_LEAF
-                const ShadeRec *hrec = tr.best != -1 ? A.shade_leaf + tr.best : nullptr;
-#elif PTG_BEST_LEAF
-                const int sid = sid_of(A, tr.best);
-                const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
-#else
                 const int sid = tr.best;
                 const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
-#endif
-                if (shade<kExact, (bool)PTG_SHADE_PACK>(hrec, tr.tb, trig, o, d, T, E, depth, st))
+                if (shade<kExact>(hrec, tr.tb, trig, o, d, T, E, depth, st))
                     path_done();
             }
             PTG_PHASE(3);
@@ -3018,7 +2099,6 @@ struct ptg_context {
     int wave_slots;     // CUs x 32 resident waves (split-tail sizing)
     LinRec *d_lin;      // linear scenes
     ShadeRec *d_shade;  // BVH scenes
-    ShadeRec *d_shade_leaf = nullptr;  // PTG_SHADE_LEAF
     void *d_bvh;  // one allocation: nodes | leaf geometry | leaf ids | big geometry | big ids
     float2 *d_trig;  // sin/cos table (trig_table)
     unsigned long long *d_acc;  // exact per-sub-pixel sums; kept zero between frames by resolve
@@ -3128,7 +2208,7 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
             g.g1 = make_float4((float)N[0], (float)N[1], (float)N[2], (float)(2.0 * R));
         } else {
             g.g0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2],
-                               PTG_SMALL_G0W ? (float)(-(R * R)) : -1.0f);
+                               (float)(-(R * R)));
             g.g1 = make_float4(0.0f, 0.0f, 0.0f, (float)(-(R * R)));
         }
         geo[i] = g;
@@ -3147,7 +2227,6 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
         int32_t mat = sp.material;
         float matf;
         std::memcpy(&matf, &mat, 4);
-#if PTG_RR_INT
         // Russian roulette as an integer compare (main.cpp:130-131, u < p):
         // u = m 2^-24 exactly (m the draw's 24-bit integer), so u < p <=> m <
         // p 2^24 <=> m < ceil(p 2^24) -- the same decisions as the oracle's
@@ -3156,12 +2235,9 @@ void prepare_scene(const ptg_sphere *s, int n, const ptg_camera *cam, std::vecto
         float p24f;
         std::memcpy(&p24f, &p24, 4);
         r.s0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], p24f);
-#else
-        r.s0 = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2], p);
-#endif
         r.s1 = make_float4((float)sp.emission[0], (float)sp.emission[1], (float)sp.emission[2], matf);
         r.s2 = make_float4(cx, cy, cz, (float)(1.0 / R));
-        r.s3 = make_float4(rx, ry, rz, PTG_RR_ROWSEL ? (float)(1.0 / R) : 0.0f);
+        r.s3 = make_float4(rx, ry, rz, (float)(1.0 / R));
         shade[i] = r;
     }
 }
@@ -3251,7 +2327,7 @@ bool outside_only(const ptg_sphere &s, const ptg_camera *cam)
     // margins: the lens bound's, the fp32 rounding of a camera origin, the
     // double rounding of d2
     const double reach = s.radius + 2.0001 * cam->lens_radius + 1e-6 * (1.0 + std::sqrt(p2)) + 1e-9 * s.radius;
-    return PTG_WALL_OUT && s.material != PTG_DIELECTRIC && d2 > reach * reach;
+    return s.material != PTG_DIELECTRIC && d2 > reach * reach;
 }
 
 void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
@@ -3414,7 +2490,7 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.count_tests = (p->flags & PTG_FLAG_COUNT_TESTS) != 0;
     A.count_nonfinite = (p->flags & PTG_FLAG_COUNT_NONFINITE) != 0;
     A.exact_math = (p->flags & PTG_FLAG_EXACT_MATH) != 0;
-    if (PTG_WALL_OUT && !A.exact_math && !A.box_walls_out)
+    if (!A.exact_math && !A.box_walls_out)
         A.box_mode = 0;  // the fast mode's box-mode wall test assumes rays outside the walls
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
@@ -3501,12 +2577,12 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
             const int nch = (nsamp + ch - 1) / ch;
             // one chunk per wave of a (linear-kernel) workgroup: the level's
             // sums stay in LDS; its first unit starts a workgroup
-            const bool coop = PTG_COOP_TAIL && ctx->n <= kLinearMax && nch == kLinWaves;
+            const bool coop = ctx->n <= kLinearMax && nch == kLinWaves;
             // BVH kernel (one wave per workgroup, no cooperative level): the
             // pixel group split into as many units of interleaved pixels,
             // each with every sample -- the unit length of nch sample chunks,
             // resolved in the wave (C5: no HBM atomics, no resolve pass)
-            const bool psplit = !coop && ctx->n > kLinearMax && PTG_BVH_TAIL_PSPLIT && l == 1 && nch > 1 &&
+            const bool psplit = !coop && ctx->n > kLinearMax && l == 1 && nch > 1 &&
                                 A.pixels_per_wave >= nch;
             if (coop)
                 A.lvl_unit[l] = (A.lvl_unit[l] + kLinWaves - 1) / kLinWaves * kLinWaves;
@@ -3664,7 +2740,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     std::vector<LinRec> lin;
     if (linear) {  // the scan's record order, interleaved, + the no-hit sentinel
         prepare_scan_order(spheres, (int)n_spheres, cam, geo, shade, axis, lgeo, lshade, order);
-        lin.resize(n_spheres + 2 + 2 * PTG_WALL_GEO);  // + the box-mode wall table(s) (scene_scan)
+        lin.resize(n_spheres + 2 + 2);  // + the box-mode wall table(s) (scene_scan)
         std::memset(lin.data(), 0, lin.size() * sizeof(LinRec));
         for (size_t i = 0; i < n_spheres; ++i)
             lin[i] = LinRec{lgeo[i], lshade[i]};
@@ -3674,7 +2750,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             walls[2 * k + 1] = order.rec_minus[k];
         }
         std::memcpy(&lin[n_spheres + 1], walls, sizeof(walls));
-#if PTG_WALL_GEO
         // entry 2 k + side: the wall's geometry, g1.x = its record's byte
         // offset; a missing wall: NaN geometry (its test never wins), offset 0
         GeoRec wg[6];
@@ -3683,8 +2758,8 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             const int off = walls[e];
             if (order.box_mode && off >= 0 && off / (int)sizeof(LinRec) < (int)n_spheres) {
                 wg[e] = lgeo[off / (int)sizeof(LinRec)];
-                // the record's byte offset (PTG_BEST_IDX: its index relative to the sentinel)
-                const int32_t tag = PTG_BEST_IDX ? off / (int)sizeof(LinRec) - (int)n_spheres : off;
+                // the record's index relative to the sentinel
+                const int32_t tag = off / (int)sizeof(LinRec) - (int)n_spheres;
                 std::memcpy(&wg[e].g1.x, &tag, 4);
             } else {
                 wg[e].g0 = make_float4(qnan, qnan, qnan, qnan);
@@ -3693,7 +2768,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         }
         static_assert(sizeof(wg) <= 2 * sizeof(LinRec), "wall geometry table size");
         std::memcpy(&lin[n_spheres + 2], wg, sizeof(wg));
-#endif
     }
     ptg_context *ctx = new ptg_context();
     ctx->device = dev;
@@ -3712,19 +2786,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_lin, lin.data(), bytes, hipMemcpyHostToDevice));
     else if (n_spheres) {
         std::vector<ShadeRec> up(shade.begin(), shade.begin() + n_spheres);
-#if PTG_SHADE_PACK
-        // s0.w = ceil(p 2^24) (<= 2^24) | material << 28 | emits << 30 (the
-        // kernel's packed reader, shade<kExact, true>)
-        static_assert(PTG_RR_INT, "the packed shading record holds the integer roulette threshold");
-        for (ShadeRec &r : up) {
-            uint32_t w, m;
-            std::memcpy(&w, &r.s0.w, 4);
-            std::memcpy(&m, &r.s1.w, 4);
-            const bool emits = r.s1.x != 0.0f || r.s1.y != 0.0f || r.s1.z != 0.0f;
-            w |= (m & 3u) << 28 | (emits ? 1u << 30 : 0u);
-            std::memcpy(&r.s0.w, &w, 4);
-        }
-#endif
         PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade, up.data(), n_spheres * sizeof(ShadeRec), hipMemcpyHostToDevice));
     }
     {
@@ -3760,18 +2821,8 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         A.plane_plus[k] = order.plane_plus[k];
         A.plane_minus[k] = order.plane_minus[k];
     }
-    A.box_mode = PTG_BOX_MODE ? order.box_mode : 0;
+    A.box_mode = order.box_mode;
     A.end_big = order.end_big;
-#if PTG_SMALL_SGPR
-    if (linear && (int)n_spheres - order.end_big == 3)
-        for (int k = 0; k < 3; ++k) {
-            const GeoRec &g = lin[order.end_big + k].g;
-            A.small_geo[k][0] = g.g0.x;
-            A.small_geo[k][1] = g.g0.y;
-            A.small_geo[k][2] = g.g0.z;
-            A.small_geo[k][3] = g.g1.w;
-        }
-#endif
     A.box_walls_out = order.box_walls_out;
     if ((int)n_spheres > kLinearMax) {
         std::vector<char> huge(n_spheres);
@@ -3786,40 +2837,20 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
         const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
-#if PTG_BVH_WIDE
         const size_t n_recs = wide_bvh(b, 0, 0).size();  // records per layout
-#else
-        const size_t n_recs = n_nodes;
-#endif
         int shift = 0;  // layout stride: a power of two > n_recs
         while ((size_t(1) << shift) <= n_recs)
             ++shift;
-#if PTG_BVH_WIDE
-        // near-plane-first boxes: one layout per octant, or one for all
-        // (PTG_BVH_ONE_LAYOUT: the kernel orders the planes per lane)
-        const size_t n_layouts = PTG_BVH_ONE_LAYOUT ? 1 : 8;
-#else
-        const size_t n_layouts = PTG_BVH_OCTANTS ? 8 : 1;
-#endif
-        // (+ PTG_BVH_LAYOUT_PAD records: the octant layouts' copies of one
-        // node are not a power of two apart)
-        const size_t stride = PTG_BVH_WIDE && PTG_BVH_INTERLEAVE
-                                  ? n_recs  // (interleaved: 8 x n_recs records in all, no layout stride)
-                                  : (size_t(1) << shift) + (PTG_BVH_WIDE ? PTG_BVH_LAYOUT_PAD : 0);
-#if PTG_BVH_Q8
-        static_assert(PTG_BVH_WIDE && PTG_BVH_INTERLEAVE && !PTG_BVH_LDS_ROOT, "48-B nodes: the interleaved wide layouts");
-        const size_t off_cont = off_q + n_layouts * (stride / kWide) * PTG_BVH_Q8_STRIDE;
-#else
+        // near-plane-first boxes: one layout per octant
+        const size_t n_layouts = 8;
+        const size_t stride = n_recs;  // (interleaved: 8 x n_recs records in all, no layout stride)
         const size_t off_cont = off_q + n_layouts * stride * sizeof(BvhNodeQ);
-#endif
-        const size_t total = off_cont + (PTG_BVH_WIDE ? n_layouts * stride / kWide * sizeof(int32_t) : 0) + 16;
+        const size_t total = off_cont + n_layouts * stride / kWide * sizeof(int32_t) + 16;
         std::vector<unsigned char> blob(total, 0);
         std::memcpy(blob.data(), b.nodes.data(), off_geo);
-#if PTG_BVH_WIDE && PTG_BVH_INTERLEAVE
         // the 8 layouts interleaved node by node: node j of layout k at
         // interleaved node 8 j + k, so the copies of one node share a 512-B
         // block instead of aliasing 2^shift records apart
-        static_assert(!PTG_BVH_ONE_LAYOUT, "interleaving needs the octant layouts");
         {
             auto ilv = [](int32_t local, int k) { return ((local >> 2) * 8 + k) * 4 + (local & 3); };
             for (int k = 0; k < 8; ++k) {
@@ -3829,60 +2860,23 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
                     BvhNodeQ &z = qk[r];
                     if (z.word >= 0)
                         z.word = ilv(z.word, k);
-#if !PTG_BVH_Q8
                     std::memcpy(blob.data() + off_q + (size_t)ilv((int32_t)r, k) * sizeof(BvhNodeQ), &z, sizeof(z));
-#endif
                 }
-#if PTG_BVH_Q8
-                // 48-B nodes: interleaved node 8 j + k at byte 48 (8 j + k)
-                for (size_t j = 0; j < qk.size() / kWide; ++j) {
-                    const WideQ8 w8 = wide_q8(&qk[j * kWide], k);
-                    std::memcpy(blob.data() + off_q + (j * 8 + (size_t)k) * PTG_BVH_Q8_STRIDE, &w8, sizeof(w8));
-                }
-#endif
                 for (size_t j = 0; j < ck.size(); ++j) {
                     const int32_t c = ck[j] >= 0 ? ilv(ck[j], k) : ck[j];
                     std::memcpy(blob.data() + off_cont + (j * 8 + (size_t)k) * sizeof(int32_t), &c, sizeof(c));
                 }
             }
         }
-        for (size_t k = 0; k < 0; ++k) {
-#else
-        for (size_t k = 0; k < n_layouts; ++k) {
-#endif
-            std::vector<BvhNodeQ> qk;
-#if PTG_BVH_WIDE
-            qk = wide_bvh(b, (int)k, (int32_t)(k * stride));  // same root box: same grid, absolute words
-            const std::vector<int32_t> ck = wide_conts(qk, (int32_t)(k * stride));
-            std::memcpy(blob.data() + off_cont + k * (stride / kWide) * sizeof(int32_t), ck.data(),
-                        ck.size() * sizeof(int32_t));
-#else
-            if (k == 0)
-                qk = qn;
-            else
-                quantise_bvh(order_bvh(b, (int)k), qk);  // same root box: same grid
-            for (BvhNodeQ &z : qk)
-                if (z.word >= 0)
-                    z.word += (int32_t)(k * stride);  // absolute skip index
-#endif
-            std::memcpy(blob.data() + off_q + k * stride * sizeof(BvhNodeQ), qk.data(), n_recs * sizeof(BvhNodeQ));
-        }
         A.bvh_shift = shift;
         A.bvh_mask = (int)(stride - 1);
-        A.bvh_oct_mask = PTG_BVH_WIDE ? 7 : PTG_BVH_OCTANTS ? bvh_octant_mask(b) : 0;
-#if PTG_BVH_WIDE
+        A.bvh_oct_mask = 7;
         const WideGrid wg(b.nodes.empty() ? BvhNodeHost{} : b.nodes[0]);
         for (int c = 0; c < 3; ++c) {
             A.q_lo[c] = wg.centre[c];
-            A.q_scale[c] = wg.scale[c] * (PTG_BVH_Q8 ? 256.0f : 1.0f);  // (48-B nodes: origins in 256-step units)
+            A.q_scale[c] = wg.scale[c];
         }
         (void)grid;
-#else
-        for (int c = 0; c < 3; ++c) {
-            A.q_lo[c] = grid.lo[c];
-            A.q_scale[c] = grid.scale[c];
-        }
-#endif
         for (size_t i = 0; i < n_leaf; ++i) {
             const ptg_sphere &sp = spheres[b.order[i]];  // leaf record {C, -R^2}, as the GeoRec of a small sphere
             const float4 rec = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2],
@@ -3909,23 +2903,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         A.big_id = reinterpret_cast<const int *>(base + off_bid);
         A.n_nodes = (int)n_recs;
         A.n_big = (int)n_big;
-#if PTG_SHADE_LEAF
-        {
-            // [n_big - 1 - k]: huge sphere k (code -2 - k); [n_big]: unused
-            // (code -1); [n_big + 1 + j]: leaf sphere j (code j)
-            std::vector<ShadeRec> sl(n_big + 1 + n_leaf);
-            for (size_t k = 0; k < n_big; ++k)
-                sl[n_big - 1 - k] = shade[b.big[k]];
-            for (size_t j = 0; j < n_leaf; ++j)
-                sl[n_big + 1 + j] = shade[b.order[j]];
-            if (hipMalloc(&ctx->d_shade_leaf, sl.size() * sizeof(ShadeRec)) != hipSuccess) {
-                ptg_context_destroy(ctx);
-                return fail(PTG_ERR_OUT_OF_MEMORY, "hipMalloc of the leaf-order shading records failed");
-            }
-            PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_shade_leaf, sl.data(), sl.size() * sizeof(ShadeRec), hipMemcpyHostToDevice));
-            A.shade_leaf = ctx->d_shade_leaf + n_big + 1;
-        }
-#endif
     }
     A.pos_x = (float)cam->position[0];
     A.pos_y = (float)cam->position[1];
@@ -3979,8 +2956,6 @@ int ptg_context_destroy(ptg_context *ctx)
         (void)hipFree(ctx->d_lin);
     if (ctx->d_shade)
         (void)hipFree(ctx->d_shade);
-    if (ctx->d_shade_leaf)
-        (void)hipFree(ctx->d_shade_leaf);
     if (ctx->d_trig)
         (void)hipFree(ctx->d_trig);
     if (ctx->d_bvh)
@@ -4025,7 +3000,7 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     if (grid <= 0)
         return PTG_OK;
     const bool bvh = A.n > kLinearMax;
-    const size_t lds = bvh ? 0 : (size_t)(A.n + 2 + 2 * PTG_WALL_GEO) * sizeof(LinRec);
+    const size_t lds = bvh ? 0 : (size_t)(A.n + 2 + 2) * sizeof(LinRec);
     // the exact mode's sin/cos table has its own LDS (render_kernel)
     const int sel = (count ? 4 : 0) | (bvh ? 2 : 0) | (A.exact_math ? 1 : 0);
     switch (sel) {

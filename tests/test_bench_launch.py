@@ -93,6 +93,10 @@ def test_group_check():
     assert bench.check_group(2, [None, None], [0, 1], ["a", "b"], False) == []
     assert bench.check_group(4, [], [0, 0, 0, 0], ["a"] * 4, True) == []
     assert bench.check_group(1, [1], [0], ["a"], False) == []
+    # unreadable bus ids (None) are not evidence either way
+    assert bench.check_group(4, [4, 4, 4, 4], [0, 1, 2, 3], [None] * 4, False) == []
+    assert bench.check_group(2, [2, 2], [None, None], [None, None], False) == []
+    assert bench.check_group(3, [3, 3, 3], [0, 1, 2], ["a", None, "a"], False) == []
 
 
 def test_launch_inprocess_flag():
