@@ -296,6 +296,8 @@ def parse_args(argv=None):
                     help="CPU baseline: time every k-th row of the frame (16 = one sixteenth)")
     ap.add_argument("--exact-math", action="store_true",
                     help="PTG_FLAG_EXACT_MATH: the exact fp32 sequences (bit for bit the CPU oracle's Mode B)")
+    ap.add_argument("--generic-scan", action="store_true",
+                    help="A/B: linear scenes on the generic scan kernel (PTG_FLAG_GENERIC_SCAN), not the box-scene one")
     ap.add_argument("--reference-f64", action="store_true",
                     help="PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode, not the metric)")
     ap.add_argument("--t1", choices=["auto", "off"], default="auto",
@@ -389,7 +391,8 @@ def bus_id_of(device):
 
 
 def arith_flags(args):
-    return (ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
+    return ((ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
+            | (ptgpu.FLAG_GENERIC_SCAN if args.generic_scan else 0))
 
 
 def arith_name(args):
@@ -400,16 +403,26 @@ def arith_name(args):
 
 def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms, n_sph, pmc):
     """S_bar*(23*N + 100) + 60 FLOP per sample for the linear
-    scan; generalised to the tests actually executed (BVH scenes): 23 FLOP per
-    ray-sphere test, 12 per slab box test, 100 per segment, 60 per sample.
-    `achieved` is one GPU's kernel: its samples x FLOP/sample / its kernel
-    time (HIP events on the launch stream)."""
+    scan (the model: every sphere tested per segment); generalised to the
+    tests actually executed for BVH scenes: 23 FLOP per ray-sphere test, 12
+    per slab box test, 100 per segment, 60 per sample.  `frac` prices the
+    model (the survey's definition); `frac_executed` prices only the tests the
+    kernel ran, from its own counters (linear scenes: box mode tests about
+    one wall and the three small spheres per segment, not all N spheres; BVH
+    scenes: the same as `frac`).  `achieved` is one GPU's kernel: its samples
+    x FLOP/sample / its kernel time (HIP events on the launch stream)."""
+    linear = n_sph <= 64
     s_bar = seg_total / frame_samples
-    tests_per_sample = sph_total / frame_samples
-    boxes_per_sample = box_total / frame_samples
-    flop_per_sample = 23 * tests_per_sample + 12 * boxes_per_sample + 100 * s_bar + 60
-    achieved = my_samples * flop_per_sample / (kern_ms / 1e3) / 1e12 if kern_ms > 0 else None
-    return s_bar, {
+    exec_tests = sph_total / frame_samples  # sphere tests executed per sample (counting kernel)
+    model_tests = s_bar * n_sph if linear else exec_tests
+    boxes = 0.0 if linear else box_total / frame_samples  # BVH box tests per sample
+    walls = box_total / frame_samples if linear else None  # linear: wall tests executed per sample
+    flop_per_sample = 23 * model_tests + 12 * boxes + 100 * s_bar + 60
+    flop_exec = 23 * exec_tests + 12 * boxes + 100 * s_bar + 60
+    tf = (lambda f: my_samples * f / (kern_ms / 1e3) / 1e12) if kern_ms > 0 else (lambda f: None)
+    achieved, achieved_exec = tf(flop_per_sample), tf(flop_exec)
+    per_seg = (lambda x: round(x / s_bar, 3) if (s_bar and x is not None) else None)
+    out = {
         "bound": "valu", "achieved": round(achieved, 3) if achieved else None,
         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4) if achieved else None,
@@ -418,26 +431,50 @@ def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms
         # MI355X_MICROARCH.md:491, and the pair moves made it 7.8 % slower)
         "peak_nonpacked": PEAK_FP32_NONPACKED_TFLOPS,
         "frac_nonpacked": round(achieved / PEAK_FP32_NONPACKED_TFLOPS, 4) if achieved else None,
-        # FP32 add/mul/fma/trans share of the VALU instructions the profile
-        # counted (the rest: compares, selects, moves, integer, converts --
-        # real issue slots the FLOP model does not count)
-        "valu_fp32_share": pmc.get("valu_fp32_share"),
-        "traffic": pmc.get("hbm_bytes_per_launch"),
+        # the tests the kernel executed (its counters), not the model's
+        "achieved_executed": round(achieved_exec, 3) if achieved_exec else None,
+        "frac_executed": round(achieved_exec / PEAK_FP32_TFLOPS, 4) if achieved_exec else None,
+        "frac_executed_nonpacked": round(achieved_exec / PEAK_FP32_NONPACKED_TFLOPS, 4) if achieved_exec else None,
         "kernel_ms": round(kern_ms, 3), "flop_per_sample": round(flop_per_sample, 1),
+        "flop_per_sample_executed": round(flop_exec, 1),
         "segments_per_sample": round(s_bar, 4),
         # SURVEY.md 8(d)'s conservative "tests-only" model: S_bar*N*23
         # (linear scenes; the BVH kernel's executed sphere tests otherwise)
-        "frac_tests_only": round(my_samples * 23 * tests_per_sample / (kern_ms / 1e3) / 1e12
-                                 / PEAK_FP32_TFLOPS, 4) if kern_ms > 0 else None,
-        "sphere_tests_per_segment": round(tests_per_sample / s_bar, 2) if s_bar else None,
-        "box_tests_per_segment": round(boxes_per_sample / s_bar, 2) if s_bar else None,
-        "scan": "bvh" if n_sph > 64 else "linear",
-        # measured issue-side view (rocprofv3 profile of this workload,
-        # profiles/<tag>_summary.json): wave64 VALU instructions x 2 cycles
-        # over the 1,024 SIMDs' cycles -- the hardware bound the FLOP model
-        # above does not see
+        "frac_tests_only": round(tf(23 * model_tests) / PEAK_FP32_TFLOPS, 4) if kern_ms > 0 else None,
+        # model: SURVEY.md 8(d)'s N tests per segment (linear); executed: the
+        # kernel's own count (for BVH scenes model = executed)
+        "model_sphere_tests_per_segment": per_seg(model_tests),
+        "sphere_tests_per_segment_executed": per_seg(exec_tests),
+        "scan": "linear" if linear else "bvh",
+    }
+    if linear:
+        out["wall_tests_per_segment_executed"] = per_seg(walls)
+    else:
+        out["box_tests_per_segment"] = per_seg(boxes)
+    # measured issue-side view (rocprofv3 profile of this workload,
+    # profiles/<tag>_summary.json): wave64 VALU instructions x 2 cycles over
+    # the 1,024 SIMDs' cycles -- the hardware bound the FLOP model does not
+    # see.  Copied from the committed profile, not measured in this run:
+    # profile_head / profile_kernel_hash say which kernel it was taken on,
+    # and profile_warning is set when that is not this tree's kernel.
+    out.update({
+        "valu_fp32_share": pmc.get("valu_fp32_share"),
+        "traffic": pmc.get("hbm_bytes_per_launch"),
         "valu_issue_pct_profiled": pmc.get("valu_issue_pct"),
-        "profile": pmc.get("tag")}
+        "profile": pmc.get("tag"),
+        "profile_head": pmc.get("commit"),
+        "profile_kernel_hash": pmc.get("kernel_hash"),
+    })
+    here = ptgpu.kernel_source_hash()
+    if pmc and pmc.get("kernel_hash") != here:
+        out["profile_warning"] = (f"valu_fp32_share / traffic / valu_issue_pct_profiled come from profile "
+                                  f"{pmc.get('tag')} (kernel {pmc.get('kernel_hash')}), not this tree's kernel ({here})")
+    return s_bar, out
+
+
+def scan_kernel_name(info):
+    """Which render kernel the frame ran (ptg_launch_info)."""
+    return "bvh" if info["bvh"] else ("box" if info.get("box_kernel") else "generic linear")
 
 
 def base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, parallelism):
@@ -546,6 +583,8 @@ def run_inprocess(args):
     value, out = base_line(args, n, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, par)
     out["segments_per_s"] = round(value * 1e6 * s_bar, 1)
     out["roofline"] = roof
+    with ptgpu.Context(scn, cam, device=0) as c0:
+        out["roofline"]["scan_kernel"] = scan_kernel_name(c0.launch_info(params))
     out["roofline"]["note"] = (f"achieved: the slowest device's kernel (device {devs[slow]}: its {dev_samples[slow]} "
                                f"samples over its HIP-event render time)")
     out["cpu_baseline"] = None
@@ -741,6 +780,7 @@ def main(argv=None):
         value, out = base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, ctx.n_spheres, elapsed, par)
         out["segments_per_s"] = round(value * 1e6 * s_bar, 1)
         out["roofline"] = roof
+        out["roofline"]["scan_kernel"] = scan_kernel_name(ctx.launch_info(params))
         cpu = None
         if world == 1 and args.cpu_baseline == "auto":
             frame = slab.cpu().numpy().reshape(rows, W, 3)[:H]  # band_rows = 1, one shard: slab row = image row

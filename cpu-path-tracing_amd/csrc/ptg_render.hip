@@ -301,6 +301,7 @@ struct KArgs {
     int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
     int count_nonfinite;           // PTG_FLAG_COUNT_NONFINITE: segments[3] += paths quant() would clip
     int exact_math;                // PTG_FLAG_EXACT_MATH: the kernels' exact arithmetic (pt_device.hpp Math)
+    int box_kernel;                // linear scenes: the box-scene instantiation applies (launch_render)
     long long n_units;
     float *out;
     unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
@@ -385,8 +386,20 @@ enum : int { kAxX = 0, kAxY = 1, kAxZ = 2, kBig = 3, kSmall = 4, kAxAny = 5, kAx
 __device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
 // Returns the winner's record, or the sentinel recs + n (no hit).
-template <bool kExact>
-__device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec *recs, f3 o, f3 d, float &tbest)
+// Tests a scan executed (counting kernels only).  BVH scenes: sphere tests
+// (huge + leaf spheres) and box tests of the walk; linear scenes: sphere
+// tests executed (walls + small spheres, each lane's own -- box mode tests
+// one wall for most rays, not all of them) and, of those, the wall tests.
+struct ScanCount {
+    uint32_t spheres = 0, boxes = 0;
+};
+
+// kBox: the box-scene instantiation (box mode, no general huge sphere,
+// exactly three small spheres -- KArgs::box_kernel); the generic scan's other
+// paths are compiled out
+template <bool kExact, bool kBox = false, bool kCount = false>
+__device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec *recs, f3 o, f3 d, float &tbest,
+                                                   ScanCount &cnt)
 {
     // the nearest root is kept as a fraction bn/bq (bq > 0); candidates are
     // compared by cross-multiplication, only the winner is divided
@@ -398,6 +411,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     auto test_geo = [&](const auto r, const float4 g0, const float4 g1, auto kind_tag, const float un = 0.0f,
                         const float vn = 0.0f, const bool valid = true, const int ks = 0) {
         constexpr int kKind = decltype(kind_tag)::value;
+        if constexpr (kCount) {
+            cnt.spheres += valid ? 1u : 0u;
+            if constexpr (kKind != kSmall)
+                cnt.boxes += valid ? 1u : 0u;  // (linear scenes: the wall tests)
+        }
         // r is wave-uniform, except for a pair's walls / box mode
         f3 e = mk3(o.x - g0.x, o.y - g0.y, o.z - g0.z);
         float ed = dot3(e, d);
@@ -543,7 +561,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     auto small_spheres = [&](int &i) {
         // three small spheres (the box scenes): straight-line code on one LDS
         // base address (the records at constant offsets), no loop control
-        if (A.n - i == 3) {
+        if (kBox || A.n - i == 3) {
             const LinRec *r0 = recs + i;
             // each record's geometry read one test ahead (its LDS latency
             // behind the previous test; the first at the scan's start)
@@ -556,10 +574,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             test_geo(-1, a2, pf_g1, std::integral_constant<int, kSmall>{});
             i = A.n;
         }
-        for (; i < A.n; ++i)
-            test(i, std::integral_constant<int, kSmall>{});
+        if constexpr (!kBox)
+            for (; i < A.n; ++i)
+                test(i, std::integral_constant<int, kSmall>{});
     };
-    if (PTG_ASSUME_BOX_MODE || A.box_mode) {
+    if (kBox || PTG_ASSUME_BOX_MODE || A.box_mode) {
         // Box mode (DESIGN.md "box mode"): per axis the wall the ray moves
         // toward and the distance u/v to its tangent plane; the wall of the
         // nearest plane is tested first.  Every wall lies beyond its tangent
@@ -689,13 +708,14 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #endif
         }
         i = A.end_ax[2];
-    } else {
+    } else if constexpr (!kBox) {
         axis_group(std::integral_constant<int, kAxX>{});
         axis_group(std::integral_constant<int, kAxY>{});
         axis_group(std::integral_constant<int, kAxZ>{});
     }
-    for (; i < A.end_big; ++i)
-        test(i, std::integral_constant<int, kBig>{});
+    if constexpr (!kBox)
+        for (; i < A.end_big; ++i)
+            test(i, std::integral_constant<int, kBig>{});
     small_spheres(i);
     tbest = bi != 0 ? Math<kExact>::div(bn, bq) : kInf;
     return recs + A.n + bi;
@@ -708,9 +728,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 // ties (main.cpp:35 strict <, in index order) -- which does not depend on the
 // visiting order, so the oracle reproduces it with a linear scan.  Box tests
 // only cull: boxes are padded (bvh_build.hpp) and use fast reciprocals.
-struct ScanCount {
-    uint32_t spheres = 0, boxes = 0;  // sphere tests and box tests of the BVH walk (counting kernel only)
-};
 
 // Root of one sphere under the reference's rule (the root >= eps nearest to
 // the origin, t = fl(num/den)); NaN when rejected or provably not below tb
@@ -1215,7 +1232,7 @@ template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st);
 
-template <bool kBvh, bool kExact, bool kCount = false>
+template <bool kBvh, bool kExact, bool kCount = false, bool kBox = false>
 __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, const float2 *trig, f3 &o, f3 &d, f3 &T,
                                         f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
 {
@@ -1225,7 +1242,7 @@ __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, cons
         const int id = scene_scan_bvh<kCount, kExact>(A, o, d, t, cnt);
         hit = id >= 0 ? A.shade + id : nullptr;
     } else {
-        const LinRec *w = scene_scan<kExact>(A, recs, o, d, t);
+        const LinRec *w = scene_scan<kExact, kBox, kCount>(A, recs, o, d, t, cnt);
         hit = w != recs + A.n ? &w->s : nullptr;
     }
     return shade<kExact>(hit, t, trig, o, d, T, E, depth, st);
@@ -1431,7 +1448,7 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // so all lanes stay busy until the pool is empty.  Path radiance is
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
-template <bool kCount, bool kBvh, bool kExact>
+template <bool kCount, bool kBvh, bool kExact, bool kBox = false>
 __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
     constexpr int kWaves = kBlockOf<kBvh> / 64;
@@ -1756,7 +1773,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if (item >= 0) {
                 if constexpr (kCount)
                     segs += 1;
-                w3 = scene_scan<kExact>(A, recs, o, d, t3);
+                w3 = scene_scan<kExact, kBox, kCount>(A, recs, o, d, t3, scnt);
             }
             lin_phase(0);
             if (item >= 0 && shade<kExact>(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st))
@@ -1769,7 +1786,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
-                if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
+                if (segment<kBvh, kExact, kCount, kBox>(A, recs, trig, o, d, T, E, depth, st, scnt))
                     path_done();
             }
             refill();
@@ -1916,7 +1933,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         if (lane_e == 0 && ws)
             atomicAdd(A.segments, ws);
         if (lane_e == 0 && A.count_tests) {
-            atomicAdd(A.segments + 1, kBvh ? wsph : ws * (unsigned long long)A.n);
+            atomicAdd(A.segments + 1, wsph);
             atomicAdd(A.segments + 2, wbox);
         }
     }
@@ -2492,6 +2509,10 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.exact_math = (p->flags & PTG_FLAG_EXACT_MATH) != 0;
     if (!A.exact_math && !A.box_walls_out)
         A.box_mode = 0;  // the fast mode's box-mode wall test assumes rays outside the walls
+    // the box-scene kernel: box mode, the walls the only huge spheres, three
+    // small spheres after them (scene_scan<kExact, true>)
+    A.box_kernel = !(p->flags & PTG_FLAG_GENERIC_SCAN) && A.n <= kLinearMax && A.box_mode &&
+                   A.end_big == A.end_ax[2] && A.n - A.end_big == 3;
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
@@ -3003,6 +3024,16 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     const size_t lds = bvh ? 0 : (size_t)(A.n + 2 + 2) * sizeof(LinRec);
     // the exact mode's sin/cos table has its own LDS (render_kernel)
     const int sel = (count ? 4 : 0) | (bvh ? 2 : 0) | (A.exact_math ? 1 : 0);
+    if (A.box_kernel && !bvh) {
+        switch (sel) {
+        case 0: render_kernel<false, false, false, true><<<grid, kBlock, lds, s>>>(A); break;
+        case 1: render_kernel<false, false, true, true><<<grid, kBlock, lds, s>>>(A); break;
+        case 4: render_kernel<true, false, false, true><<<grid, kBlock, lds, s>>>(A); break;
+        default: render_kernel<true, false, true, true><<<grid, kBlock, lds, s>>>(A); break;
+        }
+        PTG_HIP(hipGetLastError());
+        return PTG_OK;
+    }
     switch (sel) {
     case 0: render_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A); break;
     case 1: render_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A); break;
@@ -3113,7 +3144,8 @@ int ptg_launch_info(ptg_context *ctx, const ptg_params *params, int64_t *info, i
     const bool bvh = ctx->n > kLinearMax;
     const int64_t v[PTG_LAUNCH_INFO_COUNT] = {
         bvh ? 0 : A.box_mode, bvh ? 0 : A.box_walls_out, bvh ? 1 : 0, A.n_units, grid, A.n_levels,
-        A.needs_resolve ? 1 : 0, (int64_t)(A.pairs[0] | (A.pairs[1] << 1) | (A.pairs[2] << 2))};
+        A.needs_resolve ? 1 : 0, (int64_t)(A.pairs[0] | (A.pairs[1] << 1) | (A.pairs[2] << 2)),
+        bvh ? 0 : A.box_kernel};
     for (int i = 0; i < n_info; ++i)
         info[i] = i < PTG_LAUNCH_INFO_COUNT ? v[i] : 0;
     return PTG_OK;

@@ -48,6 +48,7 @@ FLAG_COUNT_TESTS = 1  # include/ptgpu.h PTG_FLAG_COUNT_TESTS
 FLAG_COUNT_NONFINITE = 2  # include/ptgpu.h PTG_FLAG_COUNT_NONFINITE (4 counters)
 FLAG_REFERENCE_F64 = 4  # include/ptgpu.h PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode)
 FLAG_EXACT_MATH = 8  # include/ptgpu.h PTG_FLAG_EXACT_MATH: exact sequences, bit for bit the oracle's Mode B
+FLAG_GENERIC_SCAN = 16  # include/ptgpu.h PTG_FLAG_GENERIC_SCAN: linear scenes on the generic scan kernel (tests, A/B)
 
 
 def _n_counters(flags: int) -> int:
@@ -225,6 +226,26 @@ class MultiContext:
         return image
 
 
+KERNEL_SOURCES = ("ptg_render.hip", "pt_device.hpp", "bvh_build.hpp")
+
+
+def kernel_source_hash() -> str:
+    """sha256 (12 hex digits) of the render kernels' sources (csrc/): names
+    the kernel a committed rocprofv3 profile was taken on (profiles/
+    summarize.py records it, bench.py compares it with this tree's)."""
+    import hashlib
+    import os
+    h = hashlib.sha256()
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+    for name in KERNEL_SOURCES:
+        try:
+            with open(os.path.join(src, name), "rb") as f:
+                h.update(f.read())
+        except OSError:
+            return "unavailable"
+    return h.hexdigest()[:12]
+
+
 def pci_bus_id(device: int) -> str:
     """ptg_device_pci_bus_id: the PCI bus id of HIP device `device`."""
     buf = C.create_string_buffer(64)
@@ -305,7 +326,7 @@ class Context:
                                       C.c_void_p(s)), "ptg_render_device")
 
     LAUNCH_INFO = ("box_mode", "box_walls_out", "bvh", "units", "workgroups", "levels", "resolve_pass",
-                   "wall_pairs")  # include/ptgpu.h ptg_launch_info
+                   "wall_pairs", "box_kernel")  # include/ptgpu.h ptg_launch_info
 
     def launch_info(self, params: Params) -> dict:
         """ptg_launch_info: how ptg_render_device would launch this frame

@@ -92,7 +92,11 @@ typedef struct ptg_params {
 
 /* flags: with PTG_FLAG_COUNT_TESTS, d_segments of ptg_render_device /
  * ptg_accumulate_device points to 3 counters: += scene scans, sphere tests
- * (ray-sphere quadratics), BVH box tests -- the inputs of the roofline model. */
+ * executed (ray-sphere quadratics), and BVH box tests (scenes of > 64
+ * spheres) or, of the sphere tests, the box-wall tests (linear scenes) --
+ * the inputs of the roofline model.  Linear scenes count each lane's own
+ * tests (box mode tests about one wall per segment, not every wall); the
+ * survey's model count is scans x spheres. */
 #define PTG_FLAG_COUNT_TESTS 1
 /* with PTG_FLAG_COUNT_NONFINITE (implies the counters above), d_segments points
  * to 4 counters; the 4th += paths whose radiance has a component that is NaN,
@@ -118,6 +122,12 @@ typedef struct ptg_params {
  * modes").  Either way a frame does not depend on sharding, work-unit sizes,
  * progressive passes or the GPU count. */
 #define PTG_FLAG_EXACT_MATH 8
+/* PTG_FLAG_GENERIC_SCAN (tests, A/B): linear scenes always run the generic
+ * scan kernel.  Without it a box scene (every huge sphere an axis wall of the
+ * box mode, exactly three small spheres: box_scene, box_mirror_scene) runs
+ * the kernel instantiated for that shape; both give the same image bit for
+ * bit. */
+#define PTG_FLAG_GENERIC_SCAN 16
 
 typedef struct ptg_context ptg_context;
 
@@ -213,9 +223,10 @@ int ptg_context_destroy(ptg_context *ctx);
  * [1] box_walls_out (no ray can start inside a box wall: the fast mode's
  * outside-only wall roots apply), [2] BVH scan (> 64 spheres), [3] work units,
  * [4] workgroups, [5] unit levels, [6] an HBM accumulator + resolve pass,
- * [7] wall-pair mask (x 1, y 2, z 4).  n_info <= PTG_LAUNCH_INFO_COUNT values
+ * [7] wall-pair mask (x 1, y 2, z 4), [8] 1 if the box-scene kernel runs
+ * (PTG_FLAG_GENERIC_SCAN).  n_info <= PTG_LAUNCH_INFO_COUNT values
  * are written (extra entries 0). */
-#define PTG_LAUNCH_INFO_COUNT 8
+#define PTG_LAUNCH_INFO_COUNT 9
 int ptg_launch_info(ptg_context *ctx, const ptg_params *params, int64_t *info, int n_info);
 
 /* Rows in one shard's slab: ceil(bands / shard_count) * band_rows. */

@@ -39,6 +39,30 @@ def per_kernel(path, kernel_sub, pick="last"):
     return val, rows, {k: [v for _, v in sorted(vs)] for k, vs in per.items()}
 
 
+def _kernel_hash():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "cpu-path-tracing_amd")]
+    try:
+        import ptgpu
+        return ptgpu.kernel_source_hash()
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def _commit():
+    """HEAD of the tree (None on the GPU box, which receives no .git: then
+    PTG_COMMIT names it, set by the launching script)."""
+    import subprocess
+    c = os.environ.get("PTG_COMMIT")
+    if c:
+        return c
+    try:
+        return subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], text=True,
+                                       stderr=subprocess.DEVNULL).strip()
+    except (OSError, subprocess.CalledProcessError):
+        return None
+
+
 def main(src, tag, kernel_sub="render_kernel"):
     out = {"tag": tag, "kernel": kernel_sub}
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
@@ -128,6 +152,9 @@ def main(src, tag, kernel_sub="render_kernel"):
     shutil.copy(stats, os.path.join(os.path.dirname(dst), f"{tag}_kernel_stats.csv"))
     rec = {"workload": out.get("bench", {}).get("config", {}).get("workload"), "tag": tag,
            "hbm_bytes_per_launch": round(fetch_b + write_b)}
+    # which kernel the profile is of (bench.py compares the hash with its tree's)
+    rec["kernel_hash"] = _kernel_hash()
+    rec["commit"] = _commit()
     if "derived" in out:
         rec["valu_issue_pct"] = round(out["derived"]["valu_issue_pct"], 1)
         rec["valu_lane_utilisation_pct"] = round(out["derived"]["VALUUtilization_pct"], 1)
