@@ -80,8 +80,14 @@ def test_image_bitexact_vs_oracle(name, W, H, samps):
     assert gsegs == rsegs
     nseg, ntest, nbox = _gpu_image.tests
     n = len(scn.spheres)
-    if n <= 64:  # linear scan: every sphere per segment, no boxes
-        assert ntest == nseg * n and nbox == 0
+    if n <= 64:
+        # linear scan: the tests each lane executed (box mode: about one wall
+        # and the three small spheres per segment), of them nbox wall tests
+        assert nseg <= ntest <= nseg * n and nbox <= ntest
+        if name == "simple":  # no wall pairs, no box mode: every sphere per segment
+            assert ntest == nseg * n
+        if name in ("box", "box_mirror"):  # box mode: 3 small spheres + >= 1 wall per segment
+            assert ntest - nbox == 3 * nseg and nseg <= nbox < 1.5 * nseg
     else:  # BVH: far fewer sphere tests than the linear scan
         assert 0 < ntest < nseg * n / 5 and nbox > 0
 
