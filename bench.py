@@ -296,10 +296,6 @@ def parse_args(argv=None):
                     help="CPU baseline: time every k-th row of the frame (16 = one sixteenth)")
     ap.add_argument("--exact-math", action="store_true",
                     help="PTG_FLAG_EXACT_MATH: the exact fp32 sequences (bit for bit the CPU oracle's Mode B)")
-    ap.add_argument("--generic-scan", action="store_true",
-                    help="A/B: linear scenes on the generic scan kernel (PTG_FLAG_GENERIC_SCAN), not the box-scene one")
-    ap.add_argument("--no-camera-packets", action="store_true",
-                    help="A/B: BVH scenes walk every camera ray per lane (PTG_FLAG_NO_CAMERA_PACKETS)")
     ap.add_argument("--reference-f64", action="store_true",
                     help="PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode, not the metric)")
     ap.add_argument("--t1", choices=["auto", "off"], default="auto",
@@ -394,8 +390,7 @@ def bus_id_of(device):
 
 def arith_flags(args):
     return ((ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
-            | (ptgpu.FLAG_GENERIC_SCAN if args.generic_scan else 0)
-            | (ptgpu.FLAG_NO_CAMERA_PACKETS if args.no_camera_packets else 0))
+)
 
 
 def arith_name(args):
@@ -478,8 +473,8 @@ def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms
 def scan_kernel_name(info):
     """Which render kernel the frame ran (ptg_launch_info)."""
     if info["bvh"]:
-        return "bvh" + (" + camera packets" if info.get("cam_packets") else "")
-    return "box" if info.get("box_kernel") else "generic linear"
+        return "bvh"
+    return "linear, box mode" if info.get("box_mode") else "linear"
 
 
 def base_line(args, world, wl_name, scene, W, H, spp, samps, nsub, n_sph, elapsed, parallelism):

@@ -301,8 +301,6 @@ struct KArgs {
     int count_tests;               // PTG_FLAG_COUNT_TESTS: segments[1..2] += sphere tests, box tests
     int count_nonfinite;           // PTG_FLAG_COUNT_NONFINITE: segments[3] += paths quant() would clip
     int exact_math;                // PTG_FLAG_EXACT_MATH: the kernels' exact arithmetic (pt_device.hpp Math)
-    int box_kernel;                // linear scenes: the box-scene instantiation applies (launch_render)
-    int cam_packets;               // BVH scenes, pinhole camera: camera rays walked as packets (packet_scan)
     long long n_units;
     float *out;
     unsigned long long *acc;  // slab_rows * W * lanes_per_pixel * 3 exact sums
@@ -395,10 +393,7 @@ struct ScanCount {
     uint32_t spheres = 0, boxes = 0;
 };
 
-// kBox: the box-scene instantiation (box mode, no general huge sphere,
-// exactly three small spheres -- KArgs::box_kernel); the generic scan's other
-// paths are compiled out
-template <bool kExact, bool kBox = false, bool kCount = false>
+template <bool kExact, bool kCount = false>
 __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec *recs, f3 o, f3 d, float &tbest,
                                                    ScanCount &cnt)
 {
@@ -562,7 +557,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     auto small_spheres = [&](int &i) {
         // three small spheres (the box scenes): straight-line code on one LDS
         // base address (the records at constant offsets), no loop control
-        if (kBox || A.n - i == 3) {
+        if (A.n - i == 3) {
             const LinRec *r0 = recs + i;
             // each record's geometry read one test ahead (its LDS latency
             // behind the previous test; the first at the scan's start)
@@ -575,11 +570,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             test_geo(-1, a2, pf_g1, std::integral_constant<int, kSmall>{});
             i = A.n;
         }
-        if constexpr (!kBox)
-            for (; i < A.n; ++i)
-                test(i, std::integral_constant<int, kSmall>{});
+        for (; i < A.n; ++i)
+            test(i, std::integral_constant<int, kSmall>{});
     };
-    if (kBox || PTG_ASSUME_BOX_MODE || A.box_mode) {
+    if (PTG_ASSUME_BOX_MODE || A.box_mode) {
         // Box mode (DESIGN.md "box mode"): per axis the wall the ray moves
         // toward and the distance u/v to its tangent plane; the wall of the
         // nearest plane is tested first.  Every wall lies beyond its tangent
@@ -709,14 +703,13 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
 #endif
         }
         i = A.end_ax[2];
-    } else if constexpr (!kBox) {
+    } else {
         axis_group(std::integral_constant<int, kAxX>{});
         axis_group(std::integral_constant<int, kAxY>{});
         axis_group(std::integral_constant<int, kAxZ>{});
     }
-    if constexpr (!kBox)
-        for (; i < A.end_big; ++i)
-            test(i, std::integral_constant<int, kBig>{});
+    for (; i < A.end_big; ++i)
+        test(i, std::integral_constant<int, kBig>{});
     small_spheres(i);
     tbest = bi != 0 ? Math<kExact>::div(bn, bq) : kInf;
     return recs + A.n + bi;
@@ -1224,117 +1217,6 @@ __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float 
     return tr.best;
 }
 
-// Camera-ray packets (DESIGN.md "camera packets").  The
-// camera rays one refill makes (up to 64: 16 neighbouring pixels x their
-// sub-pixels) leave one point when the camera is a pinhole (camera.cpp:32-38
-// with lens_radius 0: no lens offset) and are nearly parallel.  They are
-// walked as ONE wave-uniform packet: the node position is a scalar, each
-// node's 64-B line and each leaf sphere's record are read with scalar loads
-// (the scalar cache, not the vector-memory path that the per-lane walk keeps
-// 94 % busy), every lane tests the four boxes against its own ray and
-// culling distance, and a child that ANY lane hits is visited -- leaves at
-// once in near-first slot order, inner nodes through a wave-uniform LDS stack
-// (kPStack entries; the host enables packets only where 3 x the wide tree's
-// depth fits).  The lex rule (smallest t, lowest scene index on ties) does
-// not depend on the visiting order and the box culls are conservative, so
-// every lane's (t, sphere) is the per-lane walk's, bit for bit.  Rays of
-// several direction octants in one batch are walked one octant at a time
-// (each octant has its own near-plane-first layout).
-constexpr int kPStack = 48;
-template <bool kCount, bool kExact>
-__device__ __forceinline__ void packet_scan(const KArgs &A, const bool act, const f3 o, const f3 d, float &tb_out,
-                                            int &best_out, int *stk, ScanCount &cnt)
-{
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    typedef const __attribute__((address_space(4))) f32x4 *cvec_t;
-    typedef const __attribute__((address_space(4))) u32x4 *cq_t;
-    typedef const __attribute__((address_space(4))) int *cint_t;
-    const float a = dot3(d, d);
-    float tb = kInf;
-    int best = -1;
-    // the huge spheres first, linearly (as bvh_start)
-    const cvec_t bgeo = (cvec_t)A.big_geo;
-    const cint_t bid = (cint_t)A.big_id;
-    for (int k = 0; k < A.n_big; ++k) {
-        const f32x4 v0 = bgeo[2 * k], v1 = bgeo[2 * k + 1];
-        const float4 g0 = make_float4(v0.x, v0.y, v0.z, v0.w), g1 = make_float4(v1.x, v1.y, v1.z, v1.w);
-        update_lex(root_lex<true, kExact>(g0, g1, o, d, a, tb, tb * kCullScale), bid[k], tb, best);
-    }
-    if constexpr (kCount)
-        cnt.spheres += act ? (uint32_t)A.n_big : 0u;
-    const cq_t qn = (cq_t)A.bvh_qnodes;
-    const cvec_t sph = (cvec_t)A.bvh_sph;
-    const cint_t sid = (cint_t)A.bvh_id;
-    const SlabRay sr = slab_ray(A, o, d);
-    const int oct_l = (int)((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
-                            ((__float_as_uint(d.z) >> 29) & 4u));
-    unsigned long long todo = __ballot(act);
-    while (todo != 0ull) {
-        const int oct = __builtin_amdgcn_readlane(oct_l, (int)__builtin_ctzll(todo));
-        const bool mine = act & (oct_l == oct);
-        todo &= ~__ballot(mine);
-        // a leaf's spheres against every packet lane's ray (scalar loads)
-        auto leaf = [&](const int w) {
-            const int code = w & 0x7FFFFFFF;
-            const int f = code & 0xFFFFFF, nl = code >> 24;
-            if constexpr (kCount)
-                cnt.spheres += mine ? (uint32_t)nl : 0u;
-            float tbm = tb * kCullScale;
-            for (int j = 0; j < nl; ++j) {
-                const f32x4 v = sph[f + j];
-                const float t = root_lex<false, kExact>(make_float4(v.x, v.y, v.z, v.w), float4{}, o, d, a, tb, tbm);
-                update_lex(mine ? t : kReject, sid[f + j], tb, best);
-                tbm = tb * kCullScale;
-            }
-        };
-        int sp = 0;
-        int ni = oct << 2;  // layout oct's root (interleaved node oct)
-        for (;;) {
-            const u32x4 r0 = qn[ni], r1 = qn[ni + 1], r2 = qn[ni + 2], r3 = qn[ni + 3];
-            if constexpr (kCount)
-                cnt.boxes += mine ? 4u : 0u;
-            const float tcap = tb * 1.0001f;
-            const bool any0 = __ballot(mine & box_hit_sorted(r0, sr, tcap)) != 0ull;
-            const bool any1 = __ballot(mine & box_hit_sorted(r1, sr, tcap)) != 0ull;
-            const bool any2 = __ballot(mine & box_hit_sorted(r2, sr, tcap)) != 0ull;
-            const bool any3 = __ballot(mine & box_hit_sorted(r3, sr, tcap)) != 0ull;
-            const int w0 = __builtin_amdgcn_readfirstlane((int)r0.w), w1 = __builtin_amdgcn_readfirstlane((int)r1.w);
-            const int w2 = __builtin_amdgcn_readfirstlane((int)r2.w), w3 = __builtin_amdgcn_readfirstlane((int)r3.w);
-            // leaves now, in near-first slot order (an empty slot's word is -1: never hit)
-            if (any0 && w0 < kPopLater)
-                leaf(w0);
-            if (any1 && w1 < kPopLater)
-                leaf(w1);
-            if (any2 && w2 < kPopLater)
-                leaf(w2);
-            if (any3 && w3 < kPopLater)
-                leaf(w3);
-            // inner children: the nearest next, the others on the stack (far first)
-            const bool in0 = any0 && w0 >= 0, in1 = any1 && w1 >= 0, in2 = any2 && w2 >= 0, in3 = any3 && w3 >= 0;
-            int nxt = -1;
-            auto visit = [&](const bool in, const int w) {
-                if (in) {
-                    if (nxt >= 0)
-                        stk[sp++] = nxt;
-                    nxt = w;
-                }
-            };
-            visit(in3, w3);
-            visit(in2, w2);
-            visit(in1, w1);
-            visit(in0, w0);
-            if (nxt < 0) {
-                if (sp == 0)
-                    break;
-                nxt = stk[--sp];
-            }
-            ni = __builtin_amdgcn_readfirstlane(nxt);
-        }
-    }
-    tb_out = tb;
-    best_out = best;
-}
-
 // Per-lane state machine: one call = one bounce segment of radiance()
 // (main.cpp:111-155).  Returns true when the path has ended; E then holds
 // its radiance.
@@ -1344,7 +1226,7 @@ template <bool kExact>
 __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2 *trig, f3 &o, f3 &d, f3 &T, f3 &E,
                                       int &depth, uint32_t &st);
 
-template <bool kBvh, bool kExact, bool kCount = false, bool kBox = false>
+template <bool kBvh, bool kExact, bool kCount = false>
 __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, const float2 *trig, f3 &o, f3 &d, f3 &T,
                                         f3 &E, int &depth, uint32_t &st, ScanCount &cnt)
 {
@@ -1354,7 +1236,7 @@ __device__ __forceinline__ bool segment(const KArgs &A, const LinRec *recs, cons
         const int id = scene_scan_bvh<kCount, kExact>(A, o, d, t, cnt);
         hit = id >= 0 ? A.shade + id : nullptr;
     } else {
-        const LinRec *w = scene_scan<kExact, kBox, kCount>(A, recs, o, d, t, cnt);
+        const LinRec *w = scene_scan<kExact, kCount>(A, recs, o, d, t, cnt);
         hit = w != recs + A.n ? &w->s : nullptr;
     }
     return shade<kExact>(hit, t, trig, o, d, T, E, depth, st);
@@ -1560,7 +1442,7 @@ __device__ __forceinline__ unsigned long long quant(float c)
 // so all lanes stay busy until the pool is empty.  Path radiance is
 // accumulated exactly (u64) per slot in LDS and added to the global
 // accumulator once per unit.
-template <bool kCount, bool kBvh, bool kExact, bool kBox = false>
+template <bool kCount, bool kBvh, bool kExact>
 __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_kernel(KArgs A)
 {
     constexpr int kWaves = kBlockOf<kBvh> / 64;
@@ -1726,10 +1608,6 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         camera_ray(C, L, (uint32_t)sample, rs, ro, rd);
     };
     int phase = 0;  // BVH scenes: 0 fresh ray, 1 walking, 2 scan done (resumable scan, see below)
-    BvhTrav tr{};   // BVH scenes: started per segment by bvh_start (or set by a camera packet)
-    // camera packets (packet_scan): a wave-uniform stack per wave
-    __shared__ int lds_pstk[kBvh ? kWaves : 1][kBvh ? kPStack : 1];
-    const bool packets = kBvh && A.cam_packets;
     auto begin = [&](int it, f3 ro, f3 rd, uint32_t rs) {
         item = it;
         phase = 0;
@@ -1746,21 +1624,6 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         E = mk3(0.0f, 0.0f, 0.0f);
         depth = 0;
     };
-    // a camera ray whose scan a packet has done: the path starts at its
-    // first shading (the ray leaves the pinhole: o = the camera position)
-    auto begin_hit = [&](int it, f3 rd, uint32_t rs, float tb, int best) {
-        begin(it, mk3(A.pos_x, A.pos_y, A.pos_z), rd, rs);
-        phase = 2;
-        tr.tb = tb;
-        tr.best = best;
-    };
-    // packets: the record holds the scan's result where the ray's origin
-    // (the camera position) would be
-    auto store_pre_hit = [&](int it, f3 rd, uint32_t rs, float tb, int best) {
-        float4 *rec = pre_rec();
-        rec[0] = make_float4(tb, __int_as_float(best), rd.x, rd.y);
-        rec[1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), 0.0f);
-    };
     auto store_pre = [&](int it, f3 ro, f3 rd, uint32_t rs) {
         float4 *rec = pre_rec();
         rec[0] = make_float4(ro.x, ro.y, rd.x, rd.y);
@@ -1770,43 +1633,18 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         rec[1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), ro.z);
     };
     bool has_pre = false;
-    if (packets) {
-        // the unit's first 64 paths and the 64 prefetched rays: two packets
-        for (int k = 0; k < 2; ++k) {
-            const int it = k * 64 + lane;
-            f3 ro = mk3(0.0f, 0.0f, 0.0f), rd = ro;
-            uint32_t rs = 0;
-            const bool act = it < total;
-            if (act)
-                ray_of(it, ro, rd, rs);
-            float ptb;
-            int pbest;
-            packet_scan<kCount, kExact>(A, act, ro, rd, ptb, pbest, lds_pstk[kBvh ? wv : 0], scnt);
-            if constexpr (kCount)
-                segs += act ? 1u : 0u;
-            if (act) {
-                if (k == 0) {
-                    begin_hit(it, rd, rs, ptb, pbest);
-                } else {
-                    store_pre_hit(it, rd, rs, ptb, pbest);
-                    has_pre = true;
-                }
-            }
-        }
-    } else {
-        if (item >= 0) {
-            f3 ro, rd;
-            uint32_t rs;
-            ray_of(item, ro, rd, rs);
-            begin(item, ro, rd, rs);
-        }
-        if (64 + lane < total) {
-            f3 ro, rd;
-            uint32_t rs;
-            ray_of(64 + lane, ro, rd, rs);
-            store_pre(64 + lane, ro, rd, rs);
-            has_pre = true;
-        }
+    if (item >= 0) {
+        f3 ro, rd;
+        uint32_t rs;
+        ray_of(item, ro, rd, rs);
+        begin(item, ro, rd, rs);
+    }
+    if (64 + lane < total) {
+        f3 ro, rd;
+        uint32_t rs;
+        ray_of(64 + lane, ro, rd, rs);
+        store_pre(64 + lane, ro, rd, rs);
+        has_pre = true;
     }
     int next = total < 128 ? total : 128;  // wave-uniform pool cursor
     bool waiting = false;                  // path ended, no prefetched ray yet
@@ -1841,10 +1679,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             const float4 *rec = pre_rec();
             const float4 p0 = rec[0], p1 = rec[1];
             park();
-            if (packets)
-                begin_hit(__float_as_int(p1.z), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y), p0.x, __float_as_int(p0.y));
-            else
-                begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
+            begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
             has_pre = false;
         } else {
             waiting = true;  // E is kept until the batch
@@ -1871,29 +1706,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 PTG_SUB_T(rf_t1);
                 unsigned long long rf_ray = 0;
 #endif
-                if (packets) {
-                    // the batch's camera rays as one packet (packet_scan)
-                    const int ni = next + (int)__builtin_amdgcn_mbcnt_hi(
-                                              (unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-                    const bool act = !has_pre & (ni < total);
-                    f3 ro = mk3(0.0f, 0.0f, 0.0f), rd = ro;
-                    uint32_t rs = 0;
-                    if (act)
-                        ray_of(ni, ro, rd, rs);
-                    float ptb;
-                    int pbest;
-                    packet_scan<kCount, kExact>(A, act, ro, rd, ptb, pbest, lds_pstk[kBvh ? wv : 0], scnt);
-                    if constexpr (kCount)
-                        segs += act ? 1u : 0u;
-                    if (act) {
-                        if (idle) {
-                            begin_hit(ni, rd, rs, ptb, pbest);
-                        } else {
-                            store_pre_hit(ni, rd, rs, ptb, pbest);
-                            has_pre = true;
-                        }
-                    }
-                } else if (!has_pre) {
+                if (!has_pre) {
                     // lanes of need below this one (v_mbcnt: no 64-bit lane mask held in VGPRs)
                     const int ni = next + (int)__builtin_amdgcn_mbcnt_hi(
                                               (unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
@@ -1954,7 +1767,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if (item >= 0) {
                 if constexpr (kCount)
                     segs += 1;
-                w3 = scene_scan<kExact, kBox, kCount>(A, recs, o, d, t3, scnt);
+                w3 = scene_scan<kExact, kCount>(A, recs, o, d, t3, scnt);
             }
             lin_phase(0);
             if (item >= 0 && shade<kExact>(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st))
@@ -1967,7 +1780,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
-                if (segment<kBvh, kExact, kCount, kBox>(A, recs, trig, o, d, T, E, depth, st, scnt))
+                if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
                     path_done();
             }
             refill();
@@ -1983,6 +1796,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // or ready (scan done, to be shaded); an iteration starts the fresh
         // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
         // of the active lanes) or none walks, shades the ready lanes.
+        BvhTrav tr{};  // started per segment by bvh_start
 #if PTG_LEAF_SPLIT
         __shared__ uint8_t lds_pair[kWaves][2][64];  // leaf phase: owner / helper lane of each rank
 #endif
@@ -2689,12 +2503,6 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     A.exact_math = (p->flags & PTG_FLAG_EXACT_MATH) != 0;
     if (!A.exact_math && !A.box_walls_out)
         A.box_mode = 0;  // the fast mode's box-mode wall test assumes rays outside the walls
-    // the box-scene kernel: box mode, the walls the only huge spheres, three
-    // small spheres after them (scene_scan<kExact, true>)
-    A.box_kernel = !(p->flags & PTG_FLAG_GENERIC_SCAN) && A.n <= kLinearMax && A.box_mode &&
-                   A.end_big == A.end_ax[2] && A.n - A.end_big == 3;
-    if (p->flags & PTG_FLAG_NO_CAMERA_PACKETS)
-        A.cam_packets = 0;
     // work unit = pixel group x chunk of samples.  Auto: split the samples
     // only as far as needed for ~96k work units (about 16 waves per SIMD slot
     // on 256 CUs), which keeps the grid-level tail small at any GPU count.
@@ -3058,18 +2866,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             auto ilv = [](int32_t local, int k) { return ((local >> 2) * 8 + k) * 4 + (local & 3); };
             for (int k = 0; k < 8; ++k) {
                 std::vector<BvhNodeQ> qk = wide_bvh(b, k, 0);
-                if (k == 0) {
-                    // camera packets: their wave-uniform stack holds <= 3 entries
-                    // per level of the wide tree (packet_scan)
-                    std::vector<int> dep(qk.size() / 4 + 1, 1);
-                    int depth = qk.empty() ? 0 : 1;
-                    for (size_t r = qk.size(); r-- > 0;)  // children follow their parent (depth-first)
-                        if (qk[r].word >= 0 && (size_t)qk[r].word > r) {
-                            dep[r / 4] = std::max(dep[r / 4], 1 + dep[(size_t)qk[r].word / 4]);
-                            depth = std::max(depth, dep[r / 4]);
-                        }
-                    A.cam_packets = 3 * depth <= kPStack ? 1 : 0;
-                }
                 const std::vector<int32_t> ck = wide_conts(qk, 0);
                 for (size_t r = 0; r < qk.size(); ++r) {
                     BvhNodeQ &z = qk[r];
@@ -3132,7 +2928,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.Y_y = (float)cam->cam_y_axis[1];
     A.Y_z = (float)cam->cam_y_axis[2];
     A.lens = (float)cam->lens_radius;
-    A.cam_packets = A.cam_packets && !linear && cam->lens_radius == 0.0;  // a pinhole: every camera ray leaves one point
     *out = ctx;
     return PTG_OK;
 }
@@ -3219,16 +3014,6 @@ int launch_render(const KArgs &A, int grid, bool count, hipStream_t s)
     const size_t lds = bvh ? 0 : (size_t)(A.n + 2 + 2) * sizeof(LinRec);
     // the exact mode's sin/cos table has its own LDS (render_kernel)
     const int sel = (count ? 4 : 0) | (bvh ? 2 : 0) | (A.exact_math ? 1 : 0);
-    if (A.box_kernel && !bvh) {
-        switch (sel) {
-        case 0: render_kernel<false, false, false, true><<<grid, kBlock, lds, s>>>(A); break;
-        case 1: render_kernel<false, false, true, true><<<grid, kBlock, lds, s>>>(A); break;
-        case 4: render_kernel<true, false, false, true><<<grid, kBlock, lds, s>>>(A); break;
-        default: render_kernel<true, false, true, true><<<grid, kBlock, lds, s>>>(A); break;
-        }
-        PTG_HIP(hipGetLastError());
-        return PTG_OK;
-    }
     switch (sel) {
     case 0: render_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A); break;
     case 1: render_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A); break;
@@ -3339,8 +3124,7 @@ int ptg_launch_info(ptg_context *ctx, const ptg_params *params, int64_t *info, i
     const bool bvh = ctx->n > kLinearMax;
     const int64_t v[PTG_LAUNCH_INFO_COUNT] = {
         bvh ? 0 : A.box_mode, bvh ? 0 : A.box_walls_out, bvh ? 1 : 0, A.n_units, grid, A.n_levels,
-        A.needs_resolve ? 1 : 0, (int64_t)(A.pairs[0] | (A.pairs[1] << 1) | (A.pairs[2] << 2)),
-        bvh ? 0 : A.box_kernel, A.cam_packets};
+        A.needs_resolve ? 1 : 0, (int64_t)(A.pairs[0] | (A.pairs[1] << 1) | (A.pairs[2] << 2))};
     for (int i = 0; i < n_info; ++i)
         info[i] = i < PTG_LAUNCH_INFO_COUNT ? v[i] : 0;
     return PTG_OK;

@@ -48,8 +48,6 @@ FLAG_COUNT_TESTS = 1  # include/ptgpu.h PTG_FLAG_COUNT_TESTS
 FLAG_COUNT_NONFINITE = 2  # include/ptgpu.h PTG_FLAG_COUNT_NONFINITE (4 counters)
 FLAG_REFERENCE_F64 = 4  # include/ptgpu.h PTG_FLAG_REFERENCE_F64: the reference's double arithmetic (parity mode)
 FLAG_EXACT_MATH = 8  # include/ptgpu.h PTG_FLAG_EXACT_MATH: exact sequences, bit for bit the oracle's Mode B
-FLAG_GENERIC_SCAN = 16  # include/ptgpu.h PTG_FLAG_GENERIC_SCAN: linear scenes on the generic scan kernel (tests, A/B)
-FLAG_NO_CAMERA_PACKETS = 32  # include/ptgpu.h PTG_FLAG_NO_CAMERA_PACKETS: BVH camera rays walked per lane (tests, A/B)
 
 
 def _n_counters(flags: int) -> int:
@@ -327,7 +325,7 @@ class Context:
                                       C.c_void_p(s)), "ptg_render_device")
 
     LAUNCH_INFO = ("box_mode", "box_walls_out", "bvh", "units", "workgroups", "levels", "resolve_pass",
-                   "wall_pairs", "box_kernel", "cam_packets")  # include/ptgpu.h ptg_launch_info
+                   "wall_pairs")  # include/ptgpu.h ptg_launch_info
 
     def launch_info(self, params: Params) -> dict:
         """ptg_launch_info: how ptg_render_device would launch this frame

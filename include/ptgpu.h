@@ -122,17 +122,6 @@ typedef struct ptg_params {
  * modes").  Either way a frame does not depend on sharding, work-unit sizes,
  * progressive passes or the GPU count. */
 #define PTG_FLAG_EXACT_MATH 8
-/* PTG_FLAG_GENERIC_SCAN (tests, A/B): linear scenes always run the generic
- * scan kernel.  Without it a box scene (every huge sphere an axis wall of the
- * box mode, exactly three small spheres: box_scene, box_mirror_scene) runs
- * the kernel instantiated for that shape; both give the same image bit for
- * bit. */
-#define PTG_FLAG_GENERIC_SCAN 16
-/* PTG_FLAG_NO_CAMERA_PACKETS (tests, A/B): scenes of > 64 spheres walk every
- * camera ray per lane.  Without it, with a pinhole camera (lens_radius 0),
- * the camera rays of a refill batch are walked as one wave-uniform packet;
- * both give the same image bit for bit. */
-#define PTG_FLAG_NO_CAMERA_PACKETS 32
 
 typedef struct ptg_context ptg_context;
 
@@ -228,11 +217,9 @@ int ptg_context_destroy(ptg_context *ctx);
  * [1] box_walls_out (no ray can start inside a box wall: the fast mode's
  * outside-only wall roots apply), [2] BVH scan (> 64 spheres), [3] work units,
  * [4] workgroups, [5] unit levels, [6] an HBM accumulator + resolve pass,
- * [7] wall-pair mask (x 1, y 2, z 4), [8] 1 if the box-scene kernel runs
- * (PTG_FLAG_GENERIC_SCAN), [9] 1 if camera rays are walked as packets
- * (PTG_FLAG_NO_CAMERA_PACKETS).  n_info <= PTG_LAUNCH_INFO_COUNT values
+ * [7] wall-pair mask (x 1, y 2, z 4).  n_info <= PTG_LAUNCH_INFO_COUNT values
  * are written (extra entries 0). */
-#define PTG_LAUNCH_INFO_COUNT 10
+#define PTG_LAUNCH_INFO_COUNT 8
 int ptg_launch_info(ptg_context *ctx, const ptg_params *params, int64_t *info, int n_info);
 
 /* Rows in one shard's slab: ceil(bands / shard_count) * band_rows. */

@@ -291,67 +291,8 @@ def test_box_mode_fallback_is_taken():
             e = ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED, flags=EXACT))
         assert (f["box_mode"], e["box_mode"], f["box_walls_out"]) == (fast_bm, exact_bm, out), (name, f, e)
         assert f["bvh"] == 0 and f["units"] > 0 and f["workgroups"] > 0
-        # the box-scene kernel runs exactly where box mode does (these scenes
-        # have three small spheres after the walls), never under GENERIC_SCAN
-        assert (f["box_kernel"], e["box_kernel"]) == (fast_bm, exact_bm), (name, f, e)
-        with ptgpu.Context(scn, cam, device=0) as ctx:
-            g = ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED, flags=ptgpu.FLAG_GENERIC_SCAN))
-        assert g["box_kernel"] == 0 and g["box_mode"] == fast_bm, (name, g)
     scn = ptgpu.make_scene("synthetic:10000", W, H)
     cam = ptgpu.camera.with_config(scn.camera_parameters)
     with ptgpu.Context(scn, cam, device=0) as ctx:
         assert ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED))["bvh"] == 1
 
-
-@pytest.mark.parametrize("name", ["box", "box_mirror", "box_cam_near_wall"])
-@pytest.mark.parametrize("mode", [0, EXACT])
-def test_box_kernel_equals_generic_scan(name, mode):
-    """The box-scene instantiation (scene_scan<kExact, true>: box mode and
-    three small spheres compiled in, the generic scan compiled out) renders
-    the generic kernel's image bit for bit, in both arithmetic modes, with the
-    split tail of a bench-shaped frame."""
-    _require_gpu()
-    W, H, samps = 1920, 96, 8
-    scn = _scene(name, W, H)
-    cam = ptgpu.camera.with_config(scn.camera_parameters)
-    spec = _image(scn, cam, W, H, samps, flags=mode)
-    gen = _image(scn, cam, W, H, samps, flags=mode | ptgpu.FLAG_GENERIC_SCAN)
-    assert np.array_equal(spec, gen)
-
-
-@pytest.mark.parametrize("name,mode", [("synthetic:10000", 0), ("synthetic:10000", EXACT), ("synthetic:300", 0)])
-def test_camera_packets_equal_per_lane_walk(name, mode):
-    """Camera-ray packets (packet_scan: a refill batch's pinhole camera rays
-    walked as one wave-uniform packet with scalar node/leaf loads) give the
-    per-lane walk's image bit for bit: the lex rule does not depend on the
-    visiting order.  Rows of a bench-shaped frame, including its sky rows and
-    the octant changes at the image centre."""
-    _require_gpu()
-    W, H, samps = 1920, 64, 8
-    scn = ptgpu.make_scene(name, W, H)
-    cam = ptgpu.camera.with_config(scn.camera_parameters)
-    with ptgpu.Context(scn, cam, device=0) as ctx:
-        assert ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED, flags=mode))["cam_packets"] == 1
-        assert ctx.launch_info(ptgpu.make_params(W, H, samps, 2, SEED,
-                                                 flags=mode | ptgpu.FLAG_NO_CAMERA_PACKETS))["cam_packets"] == 0
-    pk = _image(scn, cam, W, H, samps, flags=mode)
-    pl = _image(scn, cam, W, H, samps, flags=mode | ptgpu.FLAG_NO_CAMERA_PACKETS)
-    assert np.array_equal(pk, pl), int((pk != pl).any(axis=2).sum())
-
-
-def test_camera_packets_only_for_pinhole_bvh_scenes():
-    """Packets need a pinhole (every camera ray leaves the camera position)
-    and a BVH scene: a thin-lens camera or a linear scene walks per lane."""
-    _require_gpu()
-    W, H = 64, 48
-    for name, want in (("box", 0), ("synthetic:300", 1)):
-        scn = ptgpu.make_scene(name, W, H)
-        cam = ptgpu.camera.with_config(scn.camera_parameters)
-        with ptgpu.Context(scn, cam, device=0) as ctx:
-            assert ctx.launch_info(ptgpu.make_params(W, H, 4, 2, SEED))["cam_packets"] == want, name
-    scn = ptgpu.make_scene("synthetic:300", W, H)
-    cfg = scn.camera_parameters
-    cfg.aperture = 0.1
-    cam = ptgpu.camera.with_config(cfg)
-    with ptgpu.Context(scn, cam, device=0) as ctx:
-        assert ctx.launch_info(ptgpu.make_params(W, H, 4, 2, SEED))["cam_packets"] == 0
