@@ -943,69 +943,15 @@ __device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, 
 // Selections are branch-free (v_cndmask).
 constexpr int kPopLater = -2;
 __device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bool need, const int keep);
-#ifndef PTG_COOP_NODES
-#define PTG_COOP_NODES 0  // A/B: node lines loaded cooperatively by the 4 lanes of a column + transposed
-#endif
-// Cooperative node load (whole wave, every lane active): the 4 lanes of a
-// column {c, c + 16, c + 32, c + 48} load the 4 nodes of the column one
-// after another, lane (row r) taking the node's 16-B record r, so each
-// wave-level load reads one 64-B line per column (16 lines, not up to 64:
-// the L1 request count that keeps the texture data path 94 % busy on C5);
-// a 4 x 4 transpose of the records across the rows (gfx950
-// v_permlane32_swap / v_permlane16_swap) gives every lane its own node.
-// base: the lane's node (first record), any valid node for a lane that does
-// not step.
-__device__ __forceinline__ void coop_node_load(gptr<u32x4> qnodes, const int base, u32x4 &q0, u32x4 &q1, u32x4 &q2,
-                                               u32x4 &q3)
-{
-    unsigned A0 = (unsigned)base, A1 = A0, A2 = A0, A3 = A0;
-    {
-        const auto r02 = __builtin_amdgcn_permlane32_swap(A0, A2, false, false);
-        const auto r13 = __builtin_amdgcn_permlane32_swap(A1, A3, false, false);
-        const auto r01 = __builtin_amdgcn_permlane16_swap(r02[0], r13[0], false, false);
-        const auto r23 = __builtin_amdgcn_permlane16_swap(r02[1], r13[1], false, false);
-        A0 = r01[0];
-        A1 = r01[1];
-        A2 = r23[0];
-        A3 = r23[1];
-    }
-    unsigned ones = ~0u;
-    asm volatile("" : "+s"(ones));
-    const unsigned row = __builtin_amdgcn_mbcnt_hi(ones, __builtin_amdgcn_mbcnt_lo(ones, 0u)) >> 4;
-    auto ld = [&](unsigned a) {
-        return *(gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + ((a + row) << 4));
-    };
-    u32x4 L0 = ld(A0), L1 = ld(A1), L2 = ld(A2), L3 = ld(A3);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const auto x02 = __builtin_amdgcn_permlane32_swap(L0[j], L2[j], false, false);
-        const auto x13 = __builtin_amdgcn_permlane32_swap(L1[j], L3[j], false, false);
-        const auto y01 = __builtin_amdgcn_permlane16_swap(x02[0], x13[0], false, false);
-        const auto y23 = __builtin_amdgcn_permlane16_swap(x02[1], x13[1], false, false);
-        L0[j] = y01[0];
-        L1[j] = y01[1];
-        L2[j] = y23[0];
-        L3[j] = y23[1];
-    }
-    q0 = L0;
-    q1 = L1;
-    q2 = L2;
-    q3 = L3;
-}
-
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r_in, BvhTrav &tr,
-                                              ScanCount &cnt, const u32x4 *pre = nullptr)
+                                              ScanCount &cnt, const u32x4 *lds_root = nullptr, int root_mask = 0,
+                                              int shift = 0)
 {
     const int base = tr.ni & ~3;
     u32x4 q0, q1, q2, q3;
     const SlabRay &r = r_in;
-    if (pre) {
-        q0 = pre[0];
-        q1 = pre[1];
-        q2 = pre[2];
-        q3 = pre[3];
-    } else {
+    {
         // a 32-bit byte offset on the uniform base: the load's saddr form
         // (no 64-bit address arithmetic per lane)
         gptr<u32x4> q = (gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + ((unsigned)base << 4));
@@ -1911,18 +1857,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         PTG_PHASE(5);
                         // (the node step as selects for the whole wave, like the
                         // leaf completion: +2.3 % -- its loads and selects for idle lanes)
-#if PTG_COOP_NODES
-                        {
-                            const bool stp = trv & (tr.pend < 0);
-                            u32x4 qq[4];
-                            coop_node_load(qnodes, stp ? (tr.ni & ~3) : 0, qq[0], qq[1], qq[2], qq[3]);
-                            if (stp)
-                                bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt, qq);
-                        }
-#else
                         if (trv && tr.pend < 0)
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
-#endif
                         PTG_PHASE(1);
                         phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
                     }
@@ -2911,7 +2847,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         const size_t off_id = off_geo + n_leaf * sizeof(float4);
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
-        const size_t off_q = (off_bid + n_big * sizeof(int) + (PTG_COOP_NODES ? 127 : 15)) & ~size_t(PTG_COOP_NODES ? 127 : 15);
+        const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
         const size_t n_recs = wide_bvh(b, 0, 0).size();  // records per layout
         int shift = 0;  // layout stride: a power of two > n_recs
         while ((size_t(1) << shift) <= n_recs)
