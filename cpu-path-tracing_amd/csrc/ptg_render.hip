@@ -192,6 +192,25 @@ __device__ unsigned long long ptg_dbg_stats2[256 * 16];
 #define PTG_STAT(i) ((void)0)
 #define PTG_PHASE(i) ((void)0)
 #endif
+#ifndef PTG_UNIT_TRACE
+#define PTG_UNIT_TRACE 0  // debug builds only: per-unit start / end wall clock and hardware id (tools/unit_trace.py)
+#endif
+#if PTG_UNIT_TRACE
+constexpr int kTraceUnits = 1 << 19;
+// unit u: [3u] start, [3u + 1] end (s_memrealtime, 100 MHz), [3u + 2] XCC id << 32 | HW_ID
+__device__ unsigned long long ptg_unit_trace[3 * kTraceUnits];
+#define PTG_TRACE_END()                                                                                \
+    do {                                                                                               \
+        if (__lane_id() == 0 && unit < kTraceUnits) {                                                  \
+            ptg_unit_trace[3 * unit] = trace_t0;                                                       \
+            ptg_unit_trace[3 * unit + 1] = wall_clock64();                                             \
+            ptg_unit_trace[3 * unit + 2] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32) | \
+                                           (unsigned long long)__builtin_amdgcn_s_getreg(0xF804);     \
+        }                                                                                              \
+    } while (0)
+#else
+#define PTG_TRACE_END() ((void)0)
+#endif
 #ifndef PTG_WAVE_STATS
 #define PTG_WAVE_STATS 0  // debug builds only: count wave-level BVH iterations instead of per-lane tests
 #endif
@@ -1509,6 +1528,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     const int s0 = A.sample_begin + (int)(coop ? t % kWaves : t / nlu) * len;
     if (s0 >= A.sample_end)
         return;  // whole wave: alignment padding before a cooperative level
+#if PTG_UNIT_TRACE
+    const unsigned long long trace_t0 = wall_clock64();
+#endif
     // the unit holds every sample of its pixels: resolve in the wave
     const bool in_wave = A.lvl_inwave[lv] != 0;
     const int slab_row = group / A.waves_per_row;
@@ -1943,8 +1965,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             prev = __hip_atomic_fetch_add(&lds_coop_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         prev = __shfl(prev, 0, 64);
         coop_last = prev == kWaves - 1;
-        if (!coop_last)
+        if (!coop_last) {
+            PTG_TRACE_END();
             return;
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     if (in_wave || coop_last) {
@@ -1989,6 +2013,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         if (vy) atomicAdd(g + 1, vy);
         if (vz) atomicAdd(g + 2, vz);
     }
+    PTG_TRACE_END();
 }
 
 // main.cpp:195-196: per pixel, the clamped sub-pixel means added with weight
@@ -2673,6 +2698,19 @@ int ptg_set_error_(int code, const char *msg) { return fail(code, msg ? msg : ""
 
 int ptg_abi_version(void) { return PTG_ABI_VERSION; }
 
+#if PTG_UNIT_TRACE
+// debug builds only: the per-unit trace of the launches since the last call
+// (3 values per unit, see ptg_unit_trace; then zeroed)
+int ptg_unit_trace_(unsigned long long *out, int n_units)
+{
+    const size_t n = (size_t)std::min(n_units, kTraceUnits) * 3;
+    PTG_HIP(hipDeviceSynchronize());
+    PTG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(ptg_unit_trace), n * sizeof(unsigned long long)));
+    std::vector<unsigned long long> z(n, 0ull);
+    PTG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ptg_unit_trace), z.data(), n * sizeof(unsigned long long)));
+    return PTG_OK;
+}
+#endif
 #if PTG_BLOCK_STATS
 // debug builds only: the 16 block counters summed over their 256 slots (then zeroed)
 int ptg_debug_stats2_(unsigned long long *out16)
