@@ -123,6 +123,9 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // scenes keep 4, the cooperative LDS-reduced level)
 #define PTG_BVH_TAIL_CHUNKS_MANY 8
 #endif
+#ifndef PTG_LIN_TAIL_HALF_ROUNDS
+#define PTG_LIN_TAIL_HALF_ROUNDS 2  // linear scenes: split-tail rows, in half rounds of the device's wave slots
+#endif
 #ifndef PTG_BVH_TAIL_HALF_ROUNDS
 #define PTG_BVH_TAIL_HALF_ROUNDS 2  // BVH scenes: split-tail rows, in half rounds of the device's wave slots
 #endif
@@ -2593,8 +2596,8 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
     // rows in PTG_TAIL_CHUNKS... chunks, see tail_level_chunks), so the last
     // units to start are the shortest.
     if (tail_ok && A.single_chunk) {
-        const long long tail_slots = ctx->n > kLinearMax ? (long long)PTG_BVH_TAIL_HALF_ROUNDS * ctx->wave_slots / 2
-                                                         : (long long)ctx->wave_slots;
+        const long long tail_slots = (long long)(ctx->n > kLinearMax ? PTG_BVH_TAIL_HALF_ROUNDS : PTG_LIN_TAIL_HALF_ROUNDS) *
+                                     ctx->wave_slots / 2;
         int tail_rows = (int)((tail_slots + A.waves_per_row - 1) / A.waves_per_row);
         tail_rows = tail_rows < A.slab_rows ? tail_rows : A.slab_rows;
         const bool many = groups >= 5LL * ctx->wave_slots;
