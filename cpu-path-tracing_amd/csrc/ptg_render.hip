@@ -123,12 +123,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // scenes keep 4, the cooperative LDS-reduced level)
 #define PTG_BVH_TAIL_CHUNKS_MANY 8
 #endif
-#ifndef PTG_SLIM_LDS
-#define PTG_SLIM_LDS 0  // A/B: linear kernel's slot table and RNG keys recomputed per camera ray (no LDS)
-#endif
-#ifndef PTG_LIN_PSPLIT
-#define PTG_LIN_PSPLIT 0  // A/B: linear scenes' split tail pixel-split (in-wave resolve) where it is not cooperative
-#endif
 #ifndef PTG_LIN_TAIL_HALF_ROUNDS
 #define PTG_LIN_TAIL_HALF_ROUNDS 2  // linear scenes: split-tail rows, in half rounds of the device's wave slots
 #endif
@@ -1475,11 +1469,8 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
 {
     constexpr int kWaves = kBlockOf<kBvh> / 64;
     __shared__ unsigned long long lds_acc[kWaves][64 * 3];
-    // PTG_SLIM_LDS (A/B, one-wave linear workgroups): the slot table and keys
-    // recomputed per camera ray instead of held in LDS (768 B per wave)
-    constexpr bool kSlim = PTG_SLIM_LDS && !kBvh;
-    __shared__ unsigned long long lds_key[kSlim ? 1 : kWaves][64];
-    __shared__ uint32_t lds_pix[kSlim ? 1 : kWaves][64];  // slot -> x | sx << 20 | sy << 26
+    __shared__ unsigned long long lds_key[kWaves][64];
+    __shared__ uint32_t lds_pix[kWaves][64];  // slot -> x | sx << 20 | sy << 26
     // sphere records staged once per workgroup in LDS (uniform-address
     // ds_read_b128 broadcasts in the scan, by-id gathers at hits); larger
     // scenes read geometry with wave-uniform scalar loads from L2/HBM instead
@@ -1562,7 +1553,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     lds_acc[wv][lane] = 0ull;
     lds_acc[wv][lane + 64] = 0ull;
     lds_acc[wv][lane + 128] = 0ull;
-    if (!kSlim && lane < nv) {
+    if (lane < nv) {
         int px = x0 + (lane / A.lanes_per_pixel) * ps;
         int sub = lane % A.lanes_per_pixel;
         int sy = sub / A.nsub;
@@ -1626,25 +1617,14 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             sample = s0 + q;
         }
         Lane L;
+        uint32_t pk = lds_pix[wv][sl];
+        L.x = (int)(pk & 0xFFFFFu);
         int yy = y;  // opaque: (float)y is converted here, not held in a VGPR for the unit
         asm volatile("" : "+s"(yy));
         L.y = yy;
-        if constexpr (kSlim) {
-            const int lpp = A.lanes_per_pixel, nsb = A.nsub;
-            const int px = x0 + (sl / lpp) * ps;
-            const int sub = sl % lpp;
-            L.x = px;
-            L.sy = sub / nsb;
-            L.sx = sub - L.sy * nsb;
-            const uint64_t pix_sub = ((uint64_t)yy * (uint64_t)A.W + (uint64_t)px) * (uint64_t)lpp + (uint64_t)sub;
-            L.key = key_hash(A.seed, pix_sub);
-        } else {
-            uint32_t pk = lds_pix[wv][sl];
-            L.x = (int)(pk & 0xFFFFFu);
-            L.sx = (int)((pk >> 20) & 63u);
-            L.sy = (int)(pk >> 26);
-            L.key = lds_key[wv][sl];
-        }
+        L.sx = (int)((pk >> 20) & 63u);
+        L.sy = (int)(pk >> 26);
+        L.key = lds_key[wv][sl];
         // the index is opaque to the compiler, so the reads stay here
         // instead of being hoisted into registers live for the whole unit
         int ci = 0;
@@ -2641,7 +2621,7 @@ int fill_launch(const ptg_context *ctx, const ptg_params *p, KArgs &A, int &grid
             // pixel group split into as many units of interleaved pixels,
             // each with every sample -- the unit length of nch sample chunks,
             // resolved in the wave (C5: no HBM atomics, no resolve pass)
-            const bool psplit = !coop && (ctx->n > kLinearMax || PTG_LIN_PSPLIT) && l == 1 && nch > 1 &&
+            const bool psplit = !coop && ctx->n > kLinearMax && l == 1 && nch > 1 &&
                                 A.pixels_per_wave >= nch;
             if (coop)
                 A.lvl_unit[l] = (A.lvl_unit[l] + kLinWaves - 1) / kLinWaves * kLinWaves;
