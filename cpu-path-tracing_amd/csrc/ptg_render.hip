@@ -123,9 +123,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // scenes keep 4, the cooperative LDS-reduced level)
 #define PTG_BVH_TAIL_CHUNKS_MANY 8
 #endif
-#ifndef PTG_LEAF_PREFETCH
-#define PTG_LEAF_PREFETCH 0  // A/B: BVH leaf loop loads the next sphere's record before testing this one
-#endif
 #ifndef PTG_LIN_TAIL_HALF_ROUNDS
 #define PTG_LIN_TAIL_HALF_ROUNDS 2  // linear scenes: split-tail rows, in half rounds of the device's wave slots
 #endif
@@ -1096,22 +1093,9 @@ __device__ __forceinline__ void leaf_spheres(const KArgs &A, int f, int cnt, f3 
     const char *sph = (const char *)A.bvh_sph;
     const char *ids = (const char *)A.bvh_id;
     float tbm = tb * kCullScale;
-#if PTG_LEAF_PREFETCH
-    // the next sphere's record loaded before this one is tested: its round
-    // trip overlaps the test (each load had been waited on at once)
-    float4 nxt = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (cnt > 0)
-        nxt = *(const float4 *)(sph + ((unsigned)f << 4));
-    for (int j = 0; j < cnt; ++j) {
-        const unsigned off = (unsigned)(f + j) << 4;
-        const float4 rec = nxt;
-        if (j + 1 < cnt)
-            nxt = *(const float4 *)(sph + off + 16);
-#else
     for (int j = 0; j < cnt; ++j) {
         const unsigned off = (unsigned)(f + j) << 4;
         const float4 rec = *(const float4 *)(sph + off);
-#endif
         const float t = root_lex<false, kExact>(rec, float4{}, o, d, a, tb, tbm);
         if (t <= tb) {  // the scene index is read only for a candidate that wins or ties
             update_lex(t, *(const int *)(ids + (off >> 2)), tb, best);
