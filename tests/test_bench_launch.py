@@ -110,3 +110,55 @@ def test_roofline_fields():
     assert abs(s_bar - 12.0) < 1e-12
     assert r["valu_fp32_share"] == 0.49
     assert abs(r["frac_nonpacked"] / r["frac"] - bench.PEAK_FP32_TFLOPS / bench.PEAK_FP32_NONPACKED_TFLOPS) < 1e-3
+
+
+def test_roofline_model_and_executed_counts():
+    """The line's roofline fields say what they count:
+    linear scenes price SURVEY 8(d)'s model (N tests per segment) in `frac`
+    and the tests the kernel executed in `frac_executed`; BVH scenes have
+    one count for both."""
+    frame = 1000
+    # linear, 8 spheres: 12 segments per sample, 4 tests executed per segment, 1 of them a wall
+    s_bar, r = bench.roofline(frame, 12 * frame, 48 * frame, 12 * frame, 2 * 10**9, 100.0, 8, {})
+    assert s_bar == 12
+    assert r["model_sphere_tests_per_segment"] == 8.0
+    assert r["sphere_tests_per_segment_executed"] == 4.0
+    assert r["wall_tests_per_segment_executed"] == 1.0
+    assert r["flop_per_sample"] == 23 * 96 + 100 * 12 + 60
+    assert r["flop_per_sample_executed"] == 23 * 48 + 100 * 12 + 60
+    assert r["frac_executed"] < r["frac"]
+    # BVH: executed sphere and box tests are the model
+    _, b = bench.roofline(frame, 2 * frame, 20 * frame, 50 * frame, 2 * 10**9, 100.0, 10000, {})
+    assert b["frac"] == b["frac_executed"] and b["box_tests_per_segment"] == 25.0
+    assert "wall_tests_per_segment_executed" not in b
+
+
+def test_roofline_profile_provenance():
+    """PMC-derived fields are copied from a committed profile: the line names
+    its tag, commit and kernel-source hash, and warns when the hash is not
+    this tree's kernel."""
+    here = bench.ptgpu.kernel_source_hash()
+    pmc = {"tag": "t", "commit": "abc1234", "kernel_hash": here, "valu_fp32_share": 0.5,
+           "hbm_bytes_per_launch": 1, "valu_issue_pct": 80.0}
+    _, r = bench.roofline(1000, 12000, 48000, 12000, 1000, 1.0, 8, pmc)
+    assert r["profile"] == "t" and r["profile_head"] == "abc1234" and r["profile_kernel_hash"] == here
+    assert "profile_warning" not in r
+    _, r = bench.roofline(1000, 12000, 48000, 12000, 1000, 1.0, 8, dict(pmc, kernel_hash="000000000000"))
+    assert "profile_warning" in r and "not this tree's kernel" in r["profile_warning"]
+
+
+def test_committed_profiles_match_the_kernel():
+    """profiles/pmc_traffic.json (what the bench line copies) was taken on
+    this tree's kernel sources."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        recs = json.load(f)
+    here = bench.ptgpu.kernel_source_hash()
+    for wl in ("box 1920x1080 1024spp", "box_mirror 1920x1080 1024spp", "synthetic:10000 1920x1080 1024spp"):
+        assert recs[wl]["kernel_hash"] == here, (wl, recs[wl].get("tag"))
+
+
+def test_scan_kernel_name():
+    assert bench.scan_kernel_name({"bvh": 1, "box_mode": 0}) == "bvh"
+    assert bench.scan_kernel_name({"bvh": 0, "box_mode": 1}) == "linear, box mode"
+    assert bench.scan_kernel_name({"bvh": 0, "box_mode": 0}) == "linear"
