@@ -123,9 +123,6 @@ static_assert(kLinearMax <= kMaxLdsSpheres, "linear scenes must fit in LDS");
 // scenes keep 4, the cooperative LDS-reduced level)
 #define PTG_BVH_TAIL_CHUNKS_MANY 8
 #endif
-#ifndef PTG_NODE_SKIP
-#define PTG_NODE_SKIP 0  // A/B: the node step loads only the records from the walk's slot on
-#endif
 #ifndef PTG_LIN_TAIL_HALF_ROUNDS
 #define PTG_LIN_TAIL_HALF_ROUNDS 2  // linear scenes: split-tail rows, in half rounds of the device's wave slots
 #endif
@@ -980,23 +977,10 @@ __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes
         // a 32-bit byte offset on the uniform base: the load's saddr form
         // (no 64-bit address arithmetic per lane)
         gptr<u32x4> q = (gptr<u32x4>)((const __attribute__((address_space(1))) char *)qnodes + ((unsigned)base << 4));
-#if PTG_NODE_SKIP
-        // records before the walk's position are not tested: not loaded either
-        const int sp = tr.ni & 3;
-        q0 = q1 = q2 = u32x4{0u, 0u, 0u, 0u};
-        if (sp == 0)
-            q0 = q[0];
-        if (sp <= 1)
-            q1 = q[1];
-        if (sp <= 2)
-            q2 = q[2];
-        q3 = q[3];
-#else
         q0 = q[0];
         q1 = q[1];
         q2 = q[2];
         q3 = q[3];
-#endif
     }
     if constexpr (kCount)
         cnt.boxes += 4 - (tr.ni & 3);
