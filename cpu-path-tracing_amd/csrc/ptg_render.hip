@@ -268,19 +268,16 @@ struct KArgs {
     int rec_plus[3], rec_minus[3];  // byte offsets of the records
     float plane_plus[3], plane_minus[3];
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
-    const float4 *bvh_nodes;  // 2 x float4 per node: {bmin, skip}, {bmax, leaf}
-    const uint4 *bvh_qnodes;  // the same nodes, compact (bvh_build.hpp BvhNodeQ; render kernel)
-    float q_lo[3], q_scale[3];  // box grid: plane = q_lo + value * q_scale (binary: u16 values; wide: binary16)
+    // the 4-wide tree (bvh_build.hpp wide_bvh): 8 near-plane-first layouts,
+    // one per ray-direction octant, interleaved node by node (node j of
+    // layout k at node 8 j + k), 4 records of 16 B per node
+    const uint4 *bvh_qnodes;
+    float q_lo[3], q_scale[3];  // box grid: plane = q_lo + value * q_scale (binary16 values)
     const float4 *bvh_sph;    // leaf-ordered spheres {C, -R^2} (BVH leaves hold only non-huge spheres)
     const int *bvh_id;        // leaf-ordered scene indices
     const GeoRec *big_geo;    // huge spheres, tested linearly
     const int *big_id;
     int n_nodes, n_big;
-    // 8 depth-first layouts of the tree (bvh_build.hpp
-    // order_bvh), layout k at node index k << bvh_shift, skip words absolute;
-    // a walk is done when (ni & bvh_mask) reaches n_nodes
-    int bvh_shift, bvh_mask;
-    int bvh_oct_mask;  // direction-sign bits that select the layout (x 1, y 2, z 4): bvh_octant_mask
     const int *bvh_cont;  // per wide node (first record / 4) its continuation (bvh_build.hpp wide_conts)
     const float2 *trig;  // {cos, sin}(2 pi k / 128), staged in LDS (sincos2pi_tab)
     // camera (camera.cpp:32-38): pos, base = llc - pos, X, Y, lens_radius
@@ -580,12 +577,8 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         // three small spheres (the box scenes): straight-line code on one LDS
         // base address (the records at constant offsets), no loop control
         if (A.n - i == 3) {
-            const LinRec *r0 = recs + i;
-            // each record's geometry read one test ahead (its LDS latency
-            // behind the previous test; the first at the scan's start)
-            const float4 a1 = r0[1].g.g0, b1 = r0[1].g.g1;
-            (void)a1;
-            (void)b1;
+            // the three records' geometry read at the scan's start (pf_g0,
+            // pf2_g0, pf3_g0: their LDS latency behind the walls' tests)
             test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
             const float4 a2 = pf3_g0;
             test_geo(-2, pf2_g0, pf_g1, std::integral_constant<int, kSmall>{});
@@ -877,7 +870,7 @@ __device__ __forceinline__ int bvh_pop(gptr<int> cont, BvhTrav &tr)
 // Start a scan: the huge spheres (tested linearly, first), then the BVH in
 // the layout of the ray's direction octant.
 template <bool kCount, bool kExact>
-__device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt, int oct_mask)
+__device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &tr, ScanCount &cnt)
 {
     const float a = dot3(d, d);
     tr.tb = kInf;
@@ -895,7 +888,7 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     if constexpr (kCount)
         cnt.spheres += A.n_big;
     // the wide layouts store each box near-plane first for their octant:
-    // all 8 layouts exist (bvh_oct_mask = 7)
+    // all 8 layouts exist
     const unsigned oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
                          ((__float_as_uint(d.z) >> 29) & 4u);
     tr.ni = A.n_nodes > 0 ? (int)(oct << 2) : -1;  // layout k's root: interleaved node k
@@ -905,7 +898,6 @@ __device__ __forceinline__ void bvh_start(const KArgs &A, f3 o, f3 d, BvhTrav &t
     tr.s2 = -1;
 #endif
     tr.res = -1;
-    (void)oct_mask;
     tr.pend = -1;
 }
 
@@ -967,8 +959,7 @@ constexpr int kPopLater = -2;
 __device__ __forceinline__ int bvh_pop_sel(gptr<int> cont, BvhTrav &tr, const bool need, const int keep);
 template <bool kCount>
 __device__ __forceinline__ void bvh_node_step(gptr<int> cont, gptr<u32x4> qnodes, const SlabRay &r_in, BvhTrav &tr,
-                                              ScanCount &cnt, const u32x4 *lds_root = nullptr, int root_mask = 0,
-                                              int shift = 0)
+                                              ScanCount &cnt)
 {
     const int base = tr.ni & ~3;
     u32x4 q0, q1, q2, q3;
@@ -1227,7 +1218,7 @@ template <bool kCount, bool kExact>
 __device__ __forceinline__ int scene_scan_bvh(const KArgs &A, f3 o, f3 d, float &tbest, ScanCount &cnt)
 {
     BvhTrav tr;
-    bvh_start<kCount, kExact>(A, o, d, tr, cnt, A.bvh_oct_mask);
+    bvh_start<kCount, kExact>(A, o, d, tr, cnt);
     const SlabRay sr = slab_ray(A, o, d);
     while (!bvh_done(A, tr)) {
         if (tr.pend >= 0)
@@ -1834,7 +1825,6 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         asm volatile("" : "+s"(cont));
         if constexpr (kExact)  // (the fast mode's sin/cos read no table)
             asm volatile("" : "+s"(trig));
-        const int oct_mask = 7;  // every octant has its layout
 #if PTG_BLOCK_STATS == 2
         unsigned long long ph_cyc[6] = {0, 0, 0, 0, 0, 0}, ph_t = clock64();
 #endif
@@ -1845,7 +1835,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if (item >= 0 && phase == 0) {
                 if constexpr (kCount)
                     segs += 1;
-                bvh_start<kCount && !PTG_WAVE_STATS, kExact>(A, o, d, tr, scnt, oct_mask);
+                bvh_start<kCount && !PTG_WAVE_STATS, kExact>(A, o, d, tr, scnt);
                 phase = bvh_done(A, tr) ? 2 : 1;
             }
             PTG_PHASE(0);
@@ -2881,28 +2871,24 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         for (size_t i = 0; i < n_spheres; ++i)
             huge[i] = is_huge(spheres[i], cam);
         BvhBuild b = build_bvh(spheres, (int)n_spheres, huge);
-        std::vector<BvhNodeQ> qn;
-        const BvhGrid grid = quantise_bvh(b.nodes, qn);
-        const size_t n_nodes = b.nodes.size(), n_leaf = b.order.size(), n_big = b.big.size();
-        const size_t off_geo = n_nodes * sizeof(BvhNodeHost);
+        const size_t n_leaf = b.order.size(), n_big = b.big.size();
+        // one allocation: leaf records | leaf ids | huge spheres | their ids |
+        // the 8 interleaved wide layouts | their continuations
+        const size_t off_geo = 0;
         const size_t off_id = off_geo + n_leaf * sizeof(float4);
         const size_t off_bgeo = (off_id + n_leaf * sizeof(int) + 15) & ~size_t(15);
         const size_t off_bid = off_bgeo + n_big * sizeof(GeoRec);
         const size_t off_q = (off_bid + n_big * sizeof(int) + 15) & ~size_t(15);
         const size_t n_recs = wide_bvh(b, 0, 0).size();  // records per layout
-        int shift = 0;  // layout stride: a power of two > n_recs
-        while ((size_t(1) << shift) <= n_recs)
-            ++shift;
         // near-plane-first boxes: one layout per octant
         const size_t n_layouts = 8;
         const size_t stride = n_recs;  // (interleaved: 8 x n_recs records in all, no layout stride)
         const size_t off_cont = off_q + n_layouts * stride * sizeof(BvhNodeQ);
         const size_t total = off_cont + n_layouts * stride / kWide * sizeof(int32_t) + 16;
         std::vector<unsigned char> blob(total, 0);
-        std::memcpy(blob.data(), b.nodes.data(), off_geo);
         // the 8 layouts interleaved node by node: node j of layout k at
         // interleaved node 8 j + k, so the copies of one node share a 512-B
-        // block instead of aliasing 2^shift records apart
+        // block instead of aliasing a power of two of records apart
         {
             auto ilv = [](int32_t local, int k) { return ((local >> 2) * 8 + k) * 4 + (local & 3); };
             for (int k = 0; k < 8; ++k) {
@@ -2920,15 +2906,11 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
                 }
             }
         }
-        A.bvh_shift = shift;
-        A.bvh_mask = (int)(stride - 1);
-        A.bvh_oct_mask = 7;
         const WideGrid wg(b.nodes.empty() ? BvhNodeHost{} : b.nodes[0]);
         for (int c = 0; c < 3; ++c) {
             A.q_lo[c] = wg.centre[c];
             A.q_scale[c] = wg.scale[c];
         }
-        (void)grid;
         for (size_t i = 0; i < n_leaf; ++i) {
             const ptg_sphere &sp = spheres[b.order[i]];  // leaf record {C, -R^2}, as the GeoRec of a small sphere
             const float4 rec = make_float4((float)sp.position[0], (float)sp.position[1], (float)sp.position[2],
@@ -2946,7 +2928,6 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
         }
         PTG_HIP_OR_DESTROY(hipMemcpy(ctx->d_bvh, blob.data(), total, hipMemcpyHostToDevice));
         unsigned char *base = static_cast<unsigned char *>(ctx->d_bvh);
-        A.bvh_nodes = reinterpret_cast<const float4 *>(base);
         A.bvh_qnodes = reinterpret_cast<const uint4 *>(base + off_q);
         A.bvh_cont = reinterpret_cast<const int *>(base + off_cont);
         A.bvh_sph = reinterpret_cast<const float4 *>(base + off_geo);
