@@ -105,14 +105,13 @@ int destroy(ptg_multi *m)
     if (!m)
         return PTG_OK;
     DeviceGuard g;
-    // every stream is drained before its buffers are freed -- a broken
-    // group's too: its communicators were aborted when the group failed, so
-    // nothing queued can block, and a failed frame's render kernels may still
-    // be running on the slabs
-    // A broken group's streams are drained with a bounded wait (ncclCommAbort
-    // should release every queued gather, but a peer that never returns must
-    // not hang close(): after ~10 s the buffers of that shard are leaked, not
-    // freed under a running kernel, and the call reports PTG_ERR_HIP).
+    // Every stream is drained before its buffers are freed -- a broken
+    // group's too, since a failed frame's render kernels may still be running
+    // on the slabs.  A broken group's communicators were aborted when the
+    // group failed, which should release every queued gather; its streams are
+    // still drained with a bounded wait, so a peer that never returns cannot
+    // hang close(): after ~10 s that shard's buffers are leaked, not freed
+    // under a running kernel, and the call reports PTG_ERR_HIP.
     int rc = PTG_OK;
     for (Shard &s : m->shards) {
         if (s.id < 0)
