@@ -389,8 +389,7 @@ def bus_id_of(device):
 
 
 def arith_flags(args):
-    return ((ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
-)
+    return (ptgpu.FLAG_REFERENCE_F64 if args.reference_f64 else 0) | (ptgpu.FLAG_EXACT_MATH if args.exact_math else 0)
 
 
 def arith_name(args):
@@ -456,6 +455,9 @@ def roofline(frame_samples, seg_total, sph_total, box_total, my_samples, kern_ms
     # profile_head / profile_kernel_hash say which kernel it was taken on,
     # and profile_warning is set when that is not this tree's kernel.
     out.update({
+        # FP32 add/mul/fma/trans share of the VALU instructions the profile
+        # counted (the rest: compares, selects, moves, integer, converts --
+        # real issue slots the FLOP model does not count)
         "valu_fp32_share": pmc.get("valu_fp32_share"),
         "traffic": pmc.get("hbm_bytes_per_launch"),
         "valu_issue_pct_profiled": pmc.get("valu_issue_pct"),
