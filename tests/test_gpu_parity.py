@@ -611,3 +611,31 @@ def test_bvh_pixel_split_tail_is_exact(samps):
     for y in (0, 1, 700):
         ref, _ = po.render_xs_rect(sp, ca, W, H, samps, 2, SEED, rows=(y, y + 1, 1), nthreads=16)
         _check_equal(tail[H - 1 - y], ref[H - 1 - y])
+
+
+def test_parameter_limits_refused_cleanly():
+    """The boundary's limits (check_params): a frame the kernel's indexing
+    does not cover is refused with an error before anything is launched,
+    and the context stays usable.  Width >= 2^20 (the slot table packs x in
+    20 bits), more than 2^28 pixels, more than 8 sub-pixels per axis, a
+    negative sample count and a shard rank outside its count."""
+    _require_gpu()
+    scn = ptgpu.make_scene("box", 64, 48)
+    cam = ptgpu.camera.with_config(scn.camera_parameters)
+    bad = [dict(w=1 << 20, h=1), dict(w=1 << 15, h=1 << 14), dict(nsub=9), dict(samps=-1),
+           dict(rank=2, count=2), dict(w=0)]
+    with ptgpu.Context(scn, cam) as ctx:
+        for b in bad:
+            p = ptgpu.make_params(b.get("w", 64), b.get("h", 48), b.get("samps", 4), b.get("nsub", 2), SEED, 1,
+                                  b.get("rank", 0), b.get("count", 1))
+            with pytest.raises(ptgpu.PtgError):
+                ctx.launch_info(p)
+        # the largest accepted shapes still plan a launch
+        for w, h, nsub in ((1 << 20) - 1, 1, 2), (1 << 14, 1 << 14, 8):
+            info = ctx.launch_info(ptgpu.make_params(w, h, 4, nsub, SEED))
+            assert info["units"] > 0 and info["workgroups"] > 0
+        # and the context still renders
+        out = torch.empty(48 * 64 * 3, dtype=torch.float32, device="cuda")
+        ctx.render_device(out, ptgpu.make_params(64, 48, 4, 2, SEED))
+        torch.cuda.synchronize()
+        assert float(out.max()) > 0.0
