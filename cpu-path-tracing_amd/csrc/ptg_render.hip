@@ -267,6 +267,11 @@ struct KArgs {
     int box_mode;
     int rec_plus[3], rec_minus[3];  // byte offsets of the records
     float plane_plus[3], plane_minus[3];
+    // box mode: -m, m > 0 the smallest gap between a wall's tangent plane and
+    // its room bound (pair_lo/hi) less a rounding margin: an origin whose
+    // plane distances up/um (scene_scan) are all >= -m lies inside the room
+    // bounds (room_neg_margin); +inf where there is no such gap
+    float room_nmr;
     // scenes with more than kLinearMax spheres: BVH (bvh_build.hpp)
     // the 4-wide tree (bvh_build.hpp wide_bvh): 8 near-plane-first layouts,
     // one per ray-direction octant, interleaved node by node (node j of
@@ -602,6 +607,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         [[maybe_unused]] const int *walls = reinterpret_cast<const int *>(recs + A.n + 1);
         float u[3], v[3];
         bool posk[3];
+        float umin = 0.0f;  // the smallest of the six plane distances (room bound check below)
         for (int k = 0; k < 3; ++k) {
             // the uniform plane / record values stay in SGPRs: select values,
             // not kernel-argument addresses (that became per-lane loads)
@@ -614,13 +620,15 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
             // wall's plane is at +-inf: u = inf is never the nearest (inf * v
             // is inf or NaN, and NaN compares false) and never needed below
             const float up = pp - comp(o, k), um = comp(o, k) - pm;
+            umin = k == 0 ? __builtin_fminf(up, um) : __builtin_fminf(__builtin_fminf(umin, up), um);
             u[k] = pos ? up : um;
             v[k] = __builtin_fabsf(dk);
             posk[k] = pos;
         }
-        // the same selection as below, kept as lane masks (is_k) and the wall
-        // table's byte offset of the selected wall (8 k, + 4 for the - wall),
-        // not as an axis index re-compared and re-multiplied
+        // the nearest plane, kept as the lane masks n1, n2 (axis 1, axis 2
+        // nearer) and the wall table's byte offset of the selected wall (8 k,
+        // + 4 for the - wall), not as an axis index re-compared and
+        // re-multiplied
         float un = u[0], vn = v[0];
         int offn = posk[0] ? 0 : 4;
         const bool n1 = u[1] * vn < un * v[1];
@@ -631,7 +639,6 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         un = n2 ? u[2] : un;
         vn = n2 ? v[2] : vn;
         offn = n2 ? (posk[2] ? 16 : 20) : offn;
-        const bool isk[3] = {!(n1 | n2), (bool)(n1 & !n2), n2};
         [[maybe_unused]] auto rec_at = [&](int off) { return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs) + off); };
         // (fast mode: box mode runs only when no ray starts inside a wall --
         // KArgs::box_walls_out -- so the outside-only roots apply)
@@ -644,24 +651,29 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
                      std::integral_constant<int, !kExact ? kAxAnyOut : kAxAny>{}, un, vn);
         }
         const float bqm = bq * kPlaneMargin;
+        // need[k]: wall k is not the selected one and its plane is not safely
+        // beyond the winner's root.  Formed as wave masks by the scalar unit
+        // from the selection's masks and one compare per plane (as per-lane
+        // logic, !n1 and !n2 had been emitted as two more compares).  A
+        // missing wall is never needed: its u is +inf, so the compare holds
+        // unless bn v is NaN, and the pass below masks a missing wall's test
+        // by its NaN geometry -- the same results
         bool need[3];
-        for (int k = 0; k < 3; ++k) {
-            // a missing wall is never needed: its u is +inf, so bn v < u bqm
-            // holds for any v (also guarded explicitly by u < inf -- a test of
-            // values: selecting the kernel-argument record offsets per lane
-            // compiled to three dependent global loads)
-            // (no u < inf guard: a missing wall's need is false unless bn v
-            // is NaN, and the pass below masks a missing wall's test by its
-            // table offset -1 -- the same results)
-            need[k] = !isk[k] & !(bn * v[k] < u[k] * bqm);
-        }
+        const unsigned long long b1 = __ballot(n1), b2 = __ballot(n2);
+        const unsigned long long nm[3] = {__ballot(!(bn * v[0] < u[0] * bqm)) & (b1 | b2),
+                                          __ballot(!(bn * v[1] < u[1] * bqm)) & (~b1 | b2),
+                                          __ballot(!(bn * v[2] < u[2] * bqm)) & ~b2};
+        for (int k = 0; k < 3; ++k)
+            need[k] = __builtin_amdgcn_inverse_ballot_w64(nm[k]);
         // a wall the ray moves away from can be hit only from beyond its
         // tangent plane (outside the room's bound on that side -- after a
         // bounce off a curved wall far from its tangent point, frequent in
-        // box_mirror's mirror tube); a missing wall's bound is +-kFarPlane
-        const bool in_room = (o.x >= A.pair_lo[0]) & (o.x <= A.pair_hi[0]) & (o.y >= A.pair_lo[1]) &
-                             (o.y <= A.pair_hi[1]) & (o.z >= A.pair_lo[2]) & (o.z <= A.pair_hi[2]);
-        if (__ballot(!in_room | need[0] | need[1] | need[2]) != 0ull) {
+        // box_mirror's mirror tube).  in_room: inside every bound, from the
+        // plane distances already formed (host room_neg_margin: it implies
+        // the six bound compares; a lane for which only those hold takes the
+        // pass below, which checks the exact bounds -- the same tests run)
+        const bool in_room = umin >= A.room_nmr;
+        if ((__ballot(!in_room) | nm[0] | nm[1] | nm[2]) != 0ull) {
             PTG_STAT(3);
 #if PTG_BLOCK_STATS == 3  // debug: wave cycles of the extra-wall block in [15]
             const unsigned long long xw_t0 = clock64();
@@ -2359,6 +2371,27 @@ bool outside_only(const ptg_sphere &s, const ptg_camera *cam)
     return s.material != PTG_DIELECTRIC && d2 > reach * reach;
 }
 
+// KArgs::room_nmr.  The kernel's up = fl(plane_plus - o_k) >= -m implies
+// plane_plus - o_k >= -m (1 + 2^-23) (a rounding of at most half an ulp of a
+// difference near -m; a larger difference passes or fails with its sign), so
+// with m = gap (1 - 2^-10) the origin lies below plane_plus + gap =
+// pair_hi; the same for um and pair_lo.  Open sides (planes at +-inf, up or
+// um = +inf) bound nothing, as their +-kFarPlane bounds (unreachable) did.
+float room_neg_margin(const KArgs &A)
+{
+    double gap = HUGE_VAL;
+    for (int k = 0; k < 3; ++k) {
+        if (A.plane_plus[k] < HUGE_VALF)
+            gap = std::min(gap, (double)A.pair_hi[k] - (double)A.plane_plus[k]);
+        if (A.plane_minus[k] > -HUGE_VALF)
+            gap = std::min(gap, (double)A.plane_minus[k] - (double)A.pair_lo[k]);
+    }
+    if (!(gap > 0.0) || gap == HUGE_VAL)
+        return HUGE_VALF;  // no lane counts as inside: every wave takes the exact per-axis checks
+    const float m = (float)(gap * (1.0 - 0x1p-10));
+    return -std::nextafter(m, 0.0f);
+}
+
 void box_mode_of(const ptg_sphere *s, int n, const ptg_camera *cam, const std::vector<int> &axis,
                  const std::vector<GeoRec> &geo, const std::vector<int> &order, KArgs &A)
 {
@@ -2866,6 +2899,7 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
     A.box_mode = order.box_mode;
     A.end_big = order.end_big;
     A.box_walls_out = order.box_walls_out;
+    A.room_nmr = room_neg_margin(A);
     if ((int)n_spheres > kLinearMax) {
         std::vector<char> huge(n_spheres);
         for (size_t i = 0; i < n_spheres; ++i)
