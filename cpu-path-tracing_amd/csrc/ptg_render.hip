@@ -425,8 +425,11 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
     // compared by cross-multiplication, only the winner is divided
     float a = dot3(d, d);
     float bn = kInf, bq = 1.0f;
-    int bi = 0;  // the winner: recs + A.n + bi (0: the sentinel, no hit)
-    auto ri_of = [&](const LinRec *r) { return (int)(r - recs) - A.n; };
+    // the winner as a byte offset from the sentinel (0: the sentinel, no
+    // hit): no multiply by the record size per segment
+    constexpr int kRecB = (int)sizeof(LinRec);
+    int bi = 0;
+    auto ri_of = [&](const LinRec *r) { return ((int)(r - recs) - A.n) * kRecB; };
     // r: the record's index relative to the sentinel
     auto test_geo = [&](const auto r, const float4 g0, const float4 g1, auto kind_tag, const float un = 0.0f,
                         const float vn = 0.0f, const bool valid = true, const int ks = 0) {
@@ -584,10 +587,10 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         if (A.n - i == 3) {
             // the three records' geometry read at the scan's start (pf_g0,
             // pf2_g0, pf3_g0: their LDS latency behind the walls' tests)
-            test_geo(-3, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
+            test_geo(-3 * kRecB, pf_g0, pf_g1, std::integral_constant<int, kSmall>{});
             const float4 a2 = pf3_g0;
-            test_geo(-2, pf2_g0, pf_g1, std::integral_constant<int, kSmall>{});
-            test_geo(-1, a2, pf_g1, std::integral_constant<int, kSmall>{});
+            test_geo(-2 * kRecB, pf2_g0, pf_g1, std::integral_constant<int, kSmall>{});
+            test_geo(-1 * kRecB, a2, pf_g1, std::integral_constant<int, kSmall>{});
             i = A.n;
         }
         for (; i < A.n; ++i)
@@ -739,7 +742,7 @@ __device__ __forceinline__ const LinRec *scene_scan(const KArgs &A, const LinRec
         test(i, std::integral_constant<int, kBig>{});
     small_spheres(i);
     tbest = bi != 0 ? Math<kExact>::div(bn, bq) : kInf;
-    return recs + A.n + bi;
+    return reinterpret_cast<const LinRec *>(reinterpret_cast<const char *>(recs + A.n) + bi);
 }
 
 // Scenes with more than kLinearMax spheres: the huge
@@ -1344,10 +1347,12 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
     f3 nd = d;  // every lane sets it below (mirror lanes in the spec block)
     // a wave with only mirror lanes skips the diffuse/dielectric work
     // (wave-uniform, exact: those lanes' values are all overwritten)
-    // (the ballot of one compare, free from its lane mask: a ballot of
-    // isD | isG was materialised as v_cndmask + v_cmp; killed lanes of
-    // those materials run the block for nothing, their values unused)
-    if (__ballot(mat != PTG_SPECULAR) != 0ull)
+    // (the active lanes less the mirror lanes' mask, which the spec compare
+    // above already formed: a ballot of isD | isG was materialised as
+    // v_cndmask + v_cmp, one of mat != PTG_SPECULAR as another compare;
+    // killed lanes of those materials run the block for nothing, their
+    // values unused)
+    if ((__ballot(1) & ~__ballot(mat == PTG_SPECULAR)) != 0ull)
     {
         PTG_STAT(4);
 #if PTG_BLOCK_STATS == 3  // debug: wave cycles of the diffuse/dielectric block in [14]
@@ -1375,7 +1380,12 @@ __device__ __forceinline__ bool shade(const ShadeRec *hit, float t, const float2
         // fast mode: one v_min_f32 (differs from the select only for NaN)
         const float cthG = kExact ? (1.0f < x0 ? 1.0f : x0) : __builtin_fminf(1.0f, x0);  // main.cpp:77
         // op2: diffuse -> sin theta = sqrt(r); dielectric -> sin theta = sqrt(1 - cos^2)
-        const float s2 = Math<kExact>::sqrt0(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
+        // (fast mode: the argument is >= 0 on every lane that reads s2 --
+        // ra >= 0, and 0 < x0 <= 1 + rounding on a dielectric lane (nn faces
+        // the ray), so cthG <= 1 and 1 - cthG^2 >= 0 -- so sqrt0's clamp of
+        // negative inputs is left out)
+        const float s2 = kExact ? Math<kExact>::sqrt0(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f))
+                                : Math<kExact>::sqrt(isD ? ra : __builtin_fmaf(-cthG, cthG, 1.0f));
         const float ratio = front ? 0.5f : 2.0f;  // main.cpp:72
         if (isG) {
             bool reflect = ratio * s2 > 1.0f;  // cannot refract: no Fresnel draw (main.cpp:89)
@@ -2833,8 +2843,9 @@ int ptg_context_create(const ptg_sphere *spheres, size_t n_spheres, const ptg_ca
             const int off = walls[e];
             if (order.box_mode && off >= 0 && off / (int)sizeof(LinRec) < (int)n_spheres) {
                 wg[e] = lgeo[off / (int)sizeof(LinRec)];
-                // the record's index relative to the sentinel
-                const int32_t tag = off / (int)sizeof(LinRec) - (int)n_spheres;
+                // the record's byte offset from the sentinel (scene_scan's
+                // winner bi)
+                const int32_t tag = (off / (int)sizeof(LinRec) - (int)n_spheres) * (int)sizeof(LinRec);
                 std::memcpy(&wg[e].g1.x, &tag, 4);
             } else {
                 wg[e].g0 = make_float4(qnan, qnan, qnan, qnan);

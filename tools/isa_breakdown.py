@@ -30,7 +30,7 @@ def func_lines(path):
     pats = {"camera_ray": r"void camera_ray\(", "scene_scan": r"const LinRec \*scene_scan\(",
             "test_rec": r"auto test_geo = ", "test_end": r"auto test_rec = ", "box_mode": r"if \(PTG_ASSUME_BOX_MODE \|\| A\.box_mode\) \{", "axis_groups": r"\} else \{\s*$",
             "box_end": r"^        i = A\.end_ax\[2\];", "shade": r"^__device__ __forceinline__ bool shade\(const ShadeRec \*hit, float t, const float2 \*trig, f3 &o, f3 &d, f3 &T, f3 &E,$",
-            "dg_block": r"if \(__ballot\(mat != PTG_SPECULAR\) != 0ull\)", "spec_block": r"if \(spec\) \{  // main.cpp:60",
+            "dg_block": r"if \(\(__ballot\(1\) & ~__ballot\(mat == PTG_SPECULAR\)\) != 0ull\)", "spec_block": r"if \(spec\) \{  // main.cpp:60",
             "ray_of": r"auto ray_of = ", "begin": r"auto begin = ", "flush": r"auto flush = ",
             "refill": r"auto refill = ", "main_loop": r"for \(;;\) \{"}
     for i, l in enumerate(src, 1):
