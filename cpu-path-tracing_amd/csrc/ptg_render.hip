@@ -1670,7 +1670,14 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // argument (a scalar load + wait in the path-start block)
         rec[1] = make_float4(rd.z, __uint_as_float(rs), __int_as_float(it), ro.z);
     };
-    bool has_pre = false;
+    // the lanes' loop state as wave masks (SGPRs, updated by the scalar unit
+    // at wave level; a lane's bit read with inverse_ballot): kept per lane,
+    // the bools lived in VGPRs and every iteration re-formed their lane masks
+    // with compares.  hmask: a prefetched ray in LDS; wmask: path ended, no
+    // prefetched ray yet (E kept until the batch); pmask: a finished path's
+    // radiance parked in the lane's LDS record
+    unsigned long long hmask = 0ull, wmask = 0ull, pmask = 0ull;
+    auto lane_in = [](unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); };
     if (item >= 0) {
         f3 ro, rd;
         uint32_t rs;
@@ -1682,10 +1689,9 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         uint32_t rs;
         ray_of(64 + lane, ro, rd, rs);
         store_pre(64 + lane, ro, rd, rs);
-        has_pre = true;
     }
+    hmask = __ballot(64 + lane < total);
     int next = total < 128 ? total : 128;  // wave-uniform pool cursor
-    bool waiting = false;                  // path ended, no prefetched ray yet
     uint32_t bad = 0;  // counting kernel: paths with a NaN / negative / > 2^30 radiance component
     auto flush = [&](float ex, float ey, float ez, int sl) {
         if constexpr (kCount)
@@ -1700,72 +1706,72 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
     // refill writes new prefetched rays there).  A lane that finishes again
     // before the batch has no prefetched ray: it waits (E in registers),
     // which forces a batch; there its E is parked, and it starts a new ray.
-    bool parked = false;
-    auto park = [&]() {
-        pre_rec()[0] = make_float4(E.x, E.y, E.z, __int_as_float(slot));
-        parked = true;
-    };
+    auto park = [&]() { pre_rec()[0] = make_float4(E.x, E.y, E.z, __int_as_float(slot)); };
     auto flush_parked = [&]() {
         const float4 pk = pre_rec()[0];
         flush(pk.x, pk.y, pk.z, __float_as_int(pk.w));
-        parked = false;
     };
-    // path end: park the radiance and start the prefetched ray, or wait
-    auto path_done = [&]() {
-        item = -1;
-        if (has_pre) {
-            const float4 *rec = pre_rec();
-            const float4 p0 = rec[0], p1 = rec[1];
-            park();
-            begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
-            has_pre = false;
-        } else {
-            waiting = true;  // E is kept until the batch
+    // path end of the lanes in done (a wave mask): park the radiance and
+    // start the prefetched ray, or wait
+    auto paths_done = [&](const unsigned long long done) {
+        if (done == 0ull)
+            return;
+        const unsigned long long start = done & hmask;
+        if (lane_in(done)) {
+            item = -1;
+            if (lane_in(start)) {
+                const float4 *rec = pre_rec();
+                const float4 p0 = rec[0], p1 = rec[1];
+                park();
+                begin(__float_as_int(p1.z), mk3(p0.x, p0.y, p1.w), mk3(p0.z, p0.w, p1.x), __float_as_uint(p1.y));
+            }
         }
+        pmask |= start;
+        hmask &= ~start;
+        wmask |= done & ~start;
     };
     // refill batch: flush parked paths, prefetch camera rays for lanes
     // without one, start idle lanes
     auto refill = [&]() {
         if (next < total) {
-            const unsigned long long need = __ballot(!has_pre);
+            const unsigned long long need = __ballot(1) & ~hmask;
             const int nn = (int)__popcll(need);
-            if (nn >= PTG_REFILL_BATCH || __ballot(waiting) != 0ull) {
+            if (nn >= PTG_REFILL_BATCH || wmask != 0ull) {
                 PTG_STAT(6);
 #if PTG_BLOCK_STATS == 3
                 PTG_SUB_T(rf_t0);
 #endif
-                const bool idle = waiting || item < 0;
-                if (parked)
+                const unsigned long long idle = wmask | __ballot(item < 0);
+                if (lane_in(pmask))
                     flush_parked();
-                if (waiting)
+                if (lane_in(wmask))
                     park();
-                waiting = false;
+                pmask = wmask;
+                wmask = 0ull;
 #if PTG_BLOCK_STATS == 3
                 PTG_SUB_T(rf_t1);
                 unsigned long long rf_ray = 0;
 #endif
-                if (!has_pre) {
-                    // lanes of need below this one (v_mbcnt: no 64-bit lane mask held in VGPRs)
-                    const int ni = next + (int)__builtin_amdgcn_mbcnt_hi(
-                                              (unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-                    if (ni < total) {
-                        f3 ro, rd;
-                        uint32_t rs;
+                // lanes of need below this one (v_mbcnt: no 64-bit lane mask held in VGPRs)
+                const int ni = next + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+                const unsigned long long got = need & __ballot(ni < total);
+                if (lane_in(got)) {
+                    f3 ro, rd;
+                    uint32_t rs;
 #if PTG_BLOCK_STATS == 3
-                        PTG_SUB_T(rr_t0);
+                    PTG_SUB_T(rr_t0);
 #endif
-                        ray_of(ni, ro, rd, rs);
+                    ray_of(ni, ro, rd, rs);
 #if PTG_BLOCK_STATS == 3
-                        rf_ray = clock64() - rr_t0;
+                    rf_ray = clock64() - rr_t0;
 #endif
-                        if (idle) {  // idle lane: start it now (its record may hold a parked path)
-                            begin(ni, ro, rd, rs);
-                        } else {
-                            store_pre(ni, ro, rd, rs);
-                            has_pre = true;
-                        }
-                    }
+                    if (lane_in(idle))  // idle lane: start it now (its record may hold a parked path)
+                        begin(ni, ro, rd, rs);
+                    else
+                        store_pre(ni, ro, rd, rs);
                 }
+                hmask |= got & ~idle;
                 next += nn;
 #if PTG_BLOCK_STATS == 3
                 {
@@ -1780,9 +1786,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 }
 #endif
             }
-        } else if (waiting) {  // pool exhausted: nothing left for this lane
-            flush(E.x, E.y, E.z, slot);
-            waiting = false;
+        } else if (wmask != 0ull) {  // pool exhausted: nothing left for this lane
+            if (lane_in(wmask))
+                flush(E.x, E.y, E.z, slot);
+            wmask = 0ull;
         }
     };
     if constexpr (!kBvh) {
@@ -1795,7 +1802,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         };
 #endif
         for (;;) {
-            if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+            if ((__ballot(item >= 0) | wmask) == 0ull)
                 break;
             PTG_STAT(0);
 #if PTG_BLOCK_STATS == 3
@@ -1808,19 +1815,19 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 w3 = scene_scan<kExact, kCount>(A, recs, o, d, t3, scnt);
             }
             lin_phase(0);
-            if (item >= 0 && shade<kExact>(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st))
-                path_done();
+            paths_done(__ballot(item >= 0 && shade<kExact>(w3 != recs + A.n ? &w3->s : nullptr, t3, trig, o, d, T, E, depth, st)));
             lin_phase(3);
             refill();
             lin_phase(4);
 #else
+            bool done = false;
             if (item >= 0) {
                 PTG_STAT(1);
                 if constexpr (kCount)
                     segs += 1;
-                if (segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt))
-                    path_done();
+                done = segment<kBvh, kExact, kCount>(A, recs, trig, o, d, T, E, depth, st, scnt);
             }
+            paths_done(__ballot(done));
             refill();
 #endif
         }
@@ -1851,7 +1858,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         unsigned long long ph_cyc[6] = {0, 0, 0, 0, 0, 0}, ph_t = clock64();
 #endif
         for (;;) {
-            if ((__ballot(item >= 0) | __ballot(waiting)) == 0ull)
+            if ((__ballot(item >= 0) | wmask) == 0ull)
                 break;
             PTG_PHASE(5);
             if (item >= 0 && phase == 0) {
@@ -1924,13 +1931,14 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             }
 #endif
             PTG_PHASE(5);
+            bool done = false;
             if (item >= 0 && phase == 2) {
                 phase = 0;
                 const int sid = tr.best;
                 const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
-                if (shade<kExact>(hrec, tr.tb, trig, o, d, T, E, depth, st))
-                    path_done();
+                done = shade<kExact>(hrec, tr.tb, trig, o, d, T, E, depth, st);
             }
+            paths_done(__ballot(done));
             PTG_PHASE(3);
             refill();
             PTG_PHASE(4);
@@ -1941,7 +1949,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                 atomicAdd(&ptg_dbg_stats[(blockIdx.x & 255) * 16 + 8 + k], ph_cyc[k]);
 #endif
     }
-    if (parked)
+    if (lane_in(pmask))
         flush_parked();
     // the lane index re-formed here (v_mbcnt of an opaque all-ones mask):
     // taken from the work-item id it was held, and spilled, through the main
