@@ -1645,10 +1645,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         const CamC C{lds_cam[ci], lds_cam[ci + 1], lds_cam[ci + 2], lds_cam[ci + 3]};
         camera_ray(C, L, (uint32_t)sample, rs, ro, rd);
     };
-    int phase = 0;  // BVH scenes: 0 fresh ray, 1 walking, 2 scan done (resumable scan, see below)
+    // (BVH scenes: a started ray is fresh -- in neither of the main loop's
+    // scan-phase masks, which its lane has left by then)
     auto begin = [&](int it, f3 ro, f3 rd, uint32_t rs) {
         item = it;
-        phase = 0;
         if (nv == 64) {
             slot = it & 63;
         } else {
@@ -1842,6 +1842,7 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
         // lanes' scans, walks until enough lanes are ready (PTG_READY_FRAC/8
         // of the active lanes) or none walks, shades the ready lanes.
         BvhTrav tr{};  // started per segment by bvh_start
+        unsigned long long wk = 0ull, rd = 0ull;  // walking / scan done (see the loop)
 #if PTG_LEAF_SPLIT
         __shared__ uint8_t lds_pair[kWaves][2][64];  // leaf phase: owner / helper lane of each rank
 #endif
@@ -1861,16 +1862,27 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
             if ((__ballot(item >= 0) | wmask) == 0ull)
                 break;
             PTG_PHASE(5);
-            if (item >= 0 && phase == 0) {
-                if constexpr (kCount)
-                    segs += 1;
-                bvh_start<kCount && !PTG_WAVE_STATS, kExact>(A, o, d, tr, scnt);
-                phase = bvh_done(A, tr) ? 2 : 1;
+            // the lanes' scan phase as wave masks (like hmask / wmask / pmask):
+            // wk walking, rd scan done (to be shaded); a fresh lane is active
+            // and in neither.  A lane's scan is done when ni == -1 and no leaf
+            // is parked: two single-compare ballots (a ballot of the combined
+            // predicate is materialised as v_cndmask + v_cmp)
+            const unsigned long long act = __ballot(item >= 0);
+            {
+                const unsigned long long fresh = act & ~(wk | rd);
+                if (lane_in(fresh)) {
+                    if constexpr (kCount)
+                        segs += 1;
+                    bvh_start<kCount && !PTG_WAVE_STATS, kExact>(A, o, d, tr, scnt);
+                }
+                const unsigned long long fin = fresh & __ballot(tr.ni == -1) & __ballot(tr.pend < 0);
+                rd |= fin;
+                wk |= fresh & ~fin;
             }
             PTG_PHASE(0);
             {
                 const SlabRay sr = slab_ray(A, o, d);
-                const int na = (int)__popcll(__ballot(item >= 0));
+                const int na = (int)__popcll(act);
                 // Node steps in an inner loop, the leaf phase in the outer one:
                 // with both in one loop body, the merge of the two branches'
                 // traversal states cost 14+ v_mov per node step (the compiler
@@ -1881,11 +1893,10 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                     for (;;) {
                         // ballots of single compares: a ballot of a combined
                         // predicate (x && y) is materialised as v_cndmask + v_cmp,
-                        // 2 VALU each.  phase 1 implies item >= 0 (an item ends
-                        // only in shading, from phase 2), and na does not change
-                        // inside the walk.
-                        const bool trv = phase == 1;
-                        const unsigned long long mt = __ballot(trv);
+                        // 2 VALU each.  A walking lane has item >= 0 (an item
+                        // ends only in shading, after the walk), and na does not
+                        // change inside the walk.
+                        const unsigned long long mt = wk;
                         const int nt = (int)__popcll(mt);
                         if (mt == 0ull || 8 * (na - nt) >= PTG_READY_FRAC * na) {
                             walk_done = true;
@@ -1901,39 +1912,47 @@ __global__ __launch_bounds__(kBlockOf<kBvh>, PTG_MIN_WAVES_PER_EU) void render_k
                         PTG_PHASE(5);
                         // (the node step as selects for the whole wave, like the
                         // leaf completion: +2.3 % -- its loads and selects for idle lanes)
-                        if (trv && tr.pend < 0)
+                        if (lane_in(mt & ~mhas))
                             bvh_node_step<kCount && !PTG_WAVE_STATS>(cont, qnodes, sr, tr, scnt);
                         PTG_PHASE(1);
-                        phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
+                        {
+                            const unsigned long long fin = wk & __ballot(tr.ni == -1) & __ballot(tr.pend < 0);
+                            rd |= fin;
+                            wk &= ~fin;
+                        }
                     }
                     if (walk_done)
                         break;
                     // leaf phase (round 1: spreading the parked leaves' spheres over
                     // the whole wave with ds_bpermute + LDS atomicMin measured 1.7 %
                     // slower; pairing idle lanes with the long leaves 1.2-1.5 % faster)
-                    const bool trv = phase == 1;
 #if PTG_LEAF_SPLIT
-                    bvh_leaf_split<kCount && !PTG_WAVE_STATS, kExact>(A, cont, o, d, trv && tr.pend >= 0, mhas, tr, scnt,
+                    bvh_leaf_split<kCount && !PTG_WAVE_STATS, kExact>(A, cont, o, d, lane_in(mhas), mhas, tr, scnt,
                                                                lds_pair[wv]);
 #else
-                    if (trv && tr.pend >= 0)
+                    if (lane_in(mhas))
                         bvh_leaf<kCount && !PTG_WAVE_STATS, kExact>(A, cont, o, d, tr, scnt);
 #endif
                     PTG_PHASE(2);
-                    phase = (trv & bvh_done(A, tr)) ? 2 : phase;  // (bitwise: && became exec-masked control flow)
+                    {
+                        const unsigned long long fin = wk & __ballot(tr.ni == -1) & __ballot(tr.pend < 0);
+                        rd |= fin;
+                        wk &= ~fin;
+                    }
                 }
             }
 #if PTG_WAVE_STATS == 2  // debug: wave-level main-loop iterations / iterations that shade (first active lane)
             if constexpr (kCount) {
                 const bool first_lane = __lane_id() == __ffsll((long long)__ballot(1)) - 1;
                 scnt.boxes += first_lane ? 1 : 0;
-                scnt.spheres += (first_lane && __ballot(item >= 0 && phase == 2) != 0ull) ? 1 : 0;
+                scnt.spheres += (first_lane && rd != 0ull) ? 1 : 0;
             }
 #endif
             PTG_PHASE(5);
             bool done = false;
-            if (item >= 0 && phase == 2) {
-                phase = 0;
+            const unsigned long long shade_m = rd;
+            rd = 0ull;
+            if (lane_in(shade_m)) {
                 const int sid = tr.best;
                 const ShadeRec *hrec = sid >= 0 ? A.shade + sid : nullptr;
                 done = shade<kExact>(hrec, tr.tb, trig, o, d, T, E, depth, st);
