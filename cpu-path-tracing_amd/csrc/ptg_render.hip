@@ -957,8 +957,11 @@ __device__ __forceinline__ bool box_hit_sorted(const u32x4 q, const SlabRay &r, 
     const float tfy = __builtin_fmaf(lo_half(q.z), r.sy, r.by);
     const float tfz = __builtin_fmaf(hi_half(q.z), r.sz, r.bz);
     const float t_in = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, 0.0f));
-    const float t_out = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, tcap));
-    return !(t_in > t_out);
+    // tcap by its own compare: as a min operand it came from outside the
+    // node step's block, so the compiler re-canonicalised it (v_max x, x) in
+    // every step; the slab times are fresh v_fma_mix results
+    const float t_out = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+    return !(t_in > t_out) & !(t_in > tcap);
 }
 
 // One wide node step at position ni (node + first slot): the node's 4
